@@ -1,0 +1,90 @@
+/*
+ * mpfft.h -- C ABI of the MI355X-native Schoenhage-Strassen multiplier
+ * (libmpfft.so, built from mpir-fft_amd/csrc/ by __graft_entry__.build()).
+ *
+ * The drop-in entry point is new_mpn_mul, with exactly the reference's
+ * signature and meaning:
+ *     /root/reference/mul_fft.c:3190-3191
+ *     void new_mpn_mul(mp_limb_t *r1, mp_limb_t *i1, mp_size_t n1,
+ *                      mp_limb_t *i2, mp_size_t n2,
+ *                      mp_bitcnt_t depth, mp_bitcnt_t w);
+ * r1[0 .. n1+n2) = i1[0 .. n1) * i2[0 .. n2), little-endian 64-bit limbs,
+ * convolution length 2^(depth+1) over Z/(2^(2^depth w) + 1).  The reference
+ * checks nothing and "will just segfault" on bad parameters
+ * (mul_fft.c:3186-3188); this library validates them and aborts with a message
+ * (new_mpn_mul) or returns a status (mpfft_mul_ex / mpfft_mul_device).
+ * The result is the exact product, bit-identical to GMP/MPIR mpn_mul and to the
+ * reference new_mpn_mul with its pointwise-row fix.
+ */
+#ifndef MPFFT_H
+#define MPFFT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#if !defined(__GMP_H__) && !defined(__MPIR_H__) && !defined(MPFFT_HAVE_MP_TYPES)
+/* GMP/MPIR LP64 types (mp_limb_t 64-bit unsigned, mp_size_t long, mp_bitcnt_t unsigned long) */
+typedef uint64_t mp_limb_t;
+typedef long mp_size_t;
+typedef unsigned long mp_bitcnt_t;
+#endif
+
+#define MPFFT_VERSION 1
+
+#define MPFFT_OK 0
+#define MPFFT_EINVAL 1          /* n1, n2 < 1; depth outside [2, 30]; n*w not a multiple of 64 */
+#define MPFFT_ETOOBIG 2         /* j1 + j2 - 1 > 2^(depth+1): product does not fit */
+#define MPFFT_EUNSUPPORTED 3    /* coefficient size n*w/64 > 4096 limbs */
+#define MPFFT_ENOMEM 4
+#define MPFFT_EHIP 5
+#define MPFFT_ENODEV 6
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Replaces new_mpn_mul, mul_fft.c:3190-3265 (host pointers; H2D, device pipeline, D2H). */
+void new_mpn_mul(mp_limb_t *r1, mp_limb_t *i1, mp_size_t n1, mp_limb_t *i2, mp_size_t n2,
+                 mp_bitcnt_t depth, mp_bitcnt_t w);
+
+/* Same as new_mpn_mul, returning MPFFT_* instead of aborting. */
+int mpfft_mul_ex(uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i2, long n2,
+                 unsigned long depth, unsigned long w);
+
+/* Device-resident multiply: all pointers are device memory, work is queued on
+ * `stream` (a hipStream_t, NULL = default) and not synchronised.  d_ws must hold
+ * mpfft_workspace_bytes(n1, n2, depth, w) bytes. */
+int mpfft_mul_device(uint64_t *d_r, const uint64_t *d_i1, long n1, const uint64_t *d_i2, long n2,
+                     unsigned long depth, unsigned long w, void *d_ws, size_t ws_bytes, void *stream);
+
+size_t mpfft_workspace_bytes(long n1, long n2, unsigned long depth, unsigned long w);
+
+/* 0 if (n1, n2, depth, w) is a valid call, else the MPFFT_* reason. */
+int mpfft_check_params(long n1, long n2, unsigned long depth, unsigned long w);
+
+/* out[10] = n, l, NC (= sqrt, columns), j1, j2, trunc, bits1, NR (rows), threads/workgroup, limbs/thread
+ * (mul_fft.c:3193-3203). */
+int mpfft_plan_info(long n1, long n2, unsigned long depth, unsigned long w, long *out);
+
+/* One stage of the pipeline on a single-GPU workspace (stage-parity tests, multi-GPU driver). */
+#define MPFFT_STAGE_FWD_COLUMNS 0   /* split + truncated column DIF, both operands   (mul_fft.c:2374-2390) */
+#define MPFFT_STAGE_FWD_ROWS 1      /* MFA twiddle + row DIF, canonical out           (mul_fft.c:2392-2408) */
+#define MPFFT_STAGE_POINTWISE 2     /* mpn_mulmod_2expp1 over the trunc live slots    (mul_fft.c:3244-3253) */
+#define MPFFT_STAGE_INV_ROWS 3      /* row DIT + MFA un-twiddle                       (mul_fft.c:2942-2957) */
+#define MPFFT_STAGE_INV_COLUMNS 4   /* truncated column inverse                       (mul_fft.c:2959-2977) */
+#define MPFFT_STAGE_SCALE 5         /* divide by 2^(depth+1), normalise               (mul_fft.c:3256-3260) */
+#define MPFFT_STAGE_COMBINE 6       /* FFT_combine_bits                               (mul_fft.c:3261-3262) */
+int mpfft_stage(int stage, const uint64_t *d_i1, const uint64_t *d_i2, uint64_t *d_r, long n1, long n2,
+                unsigned long depth, unsigned long w, void *d_ws, size_t ws_bytes, void *stream);
+
+const char *mpfft_strerror(int code);
+int mpfft_version(void);
+
+/* splitmix64-seeded xoshiro256** limbs (the benchmark's synthetic operands). */
+void mpfft_fill_random(uint64_t *buf, long cnt, uint64_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MPFFT_H */

@@ -1,0 +1,178 @@
+"""mpir-fft_amd -- MI355X-native drop-in for wbhart/mpir-fft's new_mpn_mul.
+
+Host-side mirror of the reference interface for the hot path:
+
+    new_mpn_mul(r1, i1, n1, i2, n2, depth, w)      # /root/reference/mul_fft.c:3190
+
+same names, same argument meaning (little-endian 64-bit limb arrays, convolution
+length 2^(depth+1) over Z/(2^(2^depth * w) + 1)), computed by the hand-written
+HIP kernels in csrc/ through the C ABI of libmpfft.so (include/mpfft.h).
+
+There is no CPU fallback: if libmpfft.so is missing or no GPU is visible, every
+compute entry point raises.  Errors the reference would turn into a segfault
+(mul_fft.c:3186-3188) raise MpfftError with the library's reason.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmpfft.so")
+_lib = None
+
+STAGE_FWD_COLUMNS, STAGE_FWD_ROWS, STAGE_POINTWISE, STAGE_INV_ROWS, STAGE_INV_COLUMNS, \
+    STAGE_SCALE, STAGE_COMBINE = range(7)
+
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_vp = ctypes.c_void_p
+_L = ctypes.c_long
+_UL = ctypes.c_ulong
+
+
+class MpfftError(RuntimeError):
+    def __init__(self, code, what):
+        super().__init__(f"{what}: {strerror(code)} (code {code})")
+        self.code = code
+
+
+def lib():
+    """The loaded libmpfft.so (raises if it was not built -- no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (no CPU fallback exists)")
+        # One HIP runtime per process: torch ships its own libamdhip64 (same SONAME,
+        # different file name).  Loading torch first makes libmpfft's NEEDED
+        # libamdhip64.so.7 bind to that copy, so device pointers and streams from
+        # torch are valid here; loading libmpfft first would pull in /opt/rocm's copy
+        # and a later torch import would start a second runtime that sees no device.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        h = ctypes.CDLL(LIB_PATH)
+        h.new_mpn_mul.argtypes = [_u64p, _u64p, _L, _u64p, _L, _UL, _UL]
+        h.new_mpn_mul.restype = None
+        h.mpfft_mul_ex.argtypes = [_u64p, _u64p, _L, _u64p, _L, _UL, _UL]
+        h.mpfft_mul_ex.restype = ctypes.c_int
+        h.mpfft_mul_device.argtypes = [_vp, _vp, _L, _vp, _L, _UL, _UL, _vp, ctypes.c_size_t, _vp]
+        h.mpfft_mul_device.restype = ctypes.c_int
+        h.mpfft_stage.argtypes = [ctypes.c_int, _vp, _vp, _vp, _L, _L, _UL, _UL, _vp, ctypes.c_size_t, _vp]
+        h.mpfft_stage.restype = ctypes.c_int
+        h.mpfft_workspace_bytes.argtypes = [_L, _L, _UL, _UL]
+        h.mpfft_workspace_bytes.restype = ctypes.c_size_t
+        h.mpfft_check_params.argtypes = [_L, _L, _UL, _UL]
+        h.mpfft_check_params.restype = ctypes.c_int
+        h.mpfft_plan_info.argtypes = [_L, _L, _UL, _UL, ctypes.POINTER(ctypes.c_long)]
+        h.mpfft_plan_info.restype = ctypes.c_int
+        h.mpfft_strerror.argtypes = [ctypes.c_int]
+        h.mpfft_strerror.restype = ctypes.c_char_p
+        h.mpfft_version.argtypes = []
+        h.mpfft_version.restype = ctypes.c_int
+        h.mpfft_fill_random.argtypes = [_u64p, _L, ctypes.c_uint64]
+        h.mpfft_fill_random.restype = None
+        _lib = h
+    return _lib
+
+
+def strerror(code):
+    return lib().mpfft_strerror(int(code)).decode()
+
+
+def _p(a):
+    if a.dtype != np.uint64 or not a.flags["C_CONTIGUOUS"]:
+        raise TypeError("limb arrays must be C-contiguous numpy.uint64")
+    return a.ctypes.data_as(_u64p)
+
+
+def check_params(n1, n2, depth, w):
+    return lib().mpfft_check_params(n1, n2, depth, w)
+
+
+def plan_info(n1, n2, depth, w):
+    """dict of the derived parameters (mul_fft.c:3193-3203) or MpfftError."""
+    out = (ctypes.c_long * 10)()
+    rc = lib().mpfft_plan_info(n1, n2, depth, w, out)
+    if rc:
+        raise MpfftError(rc, f"plan(n1={n1}, n2={n2}, depth={depth}, w={w})")
+    keys = ("n", "l", "NC", "j1", "j2", "trunc", "bits1", "NR", "tpb", "U")
+    return dict(zip(keys, list(out)))
+
+
+def workspace_bytes(n1, n2, depth, w):
+    return int(lib().mpfft_workspace_bytes(n1, n2, depth, w))
+
+
+def new_mpn_mul(r1, i1, n1, i2, n2, depth, w):
+    """Reference-shaped entry (mul_fft.c:3190): r1[:n1+n2] = i1[:n1] * i2[:n2]."""
+    if len(r1) < n1 + n2 or len(i1) < n1 or len(i2) < n2:
+        raise ValueError("buffer shorter than the stated limb count")
+    rc = lib().mpfft_mul_ex(_p(r1), _p(i1), n1, _p(i2), n2, depth, w)
+    if rc:
+        raise MpfftError(rc, f"new_mpn_mul(n1={n1}, n2={n2}, depth={depth}, w={w})")
+
+
+def mul(i1, i2, depth, w):
+    """Convenience: returns the n1+n2 limb product as a new uint64 array."""
+    i1 = np.ascontiguousarray(i1, dtype=np.uint64)
+    i2 = np.ascontiguousarray(i2, dtype=np.uint64)
+    r = np.zeros(len(i1) + len(i2), dtype=np.uint64)
+    new_mpn_mul(r, i1, len(i1), i2, len(i2), depth, w)
+    return r
+
+
+def fill_random(count, seed):
+    buf = np.empty(count, dtype=np.uint64)
+    lib().mpfft_fill_random(_p(buf), count, seed)
+    return buf
+
+
+# ---- device-resident entry points (torch tensors as HBM plumbing) ----------
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream(stream):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def alloc_workspace(n1, n2, depth, w, device="cuda"):
+    import torch
+    nb = workspace_bytes(n1, n2, depth, w)
+    if nb == 0:
+        raise MpfftError(check_params(n1, n2, depth, w), "workspace")
+    return torch.empty(nb, dtype=torch.uint8, device=device)
+
+
+def mul_device(d_r, d_i1, n1, d_i2, n2, depth, w, ws, stream=None):
+    """All tensors on the GPU (int64/uint64 limbs); queued on `stream`, not synchronised."""
+    rc = lib().mpfft_mul_device(_ptr(d_r), _ptr(d_i1), n1, _ptr(d_i2), n2, depth, w, _ptr(ws),
+                                ws.numel() * ws.element_size(), _stream(stream))
+    if rc:
+        raise MpfftError(rc, "mpfft_mul_device")
+
+
+def stage(which, d_i1, d_i2, d_r, n1, n2, depth, w, ws, stream=None):
+    rc = lib().mpfft_stage(which, _ptr(d_i1), _ptr(d_i2), _ptr(d_r), n1, n2, depth, w, _ptr(ws),
+                           ws.numel() * ws.element_size(), _stream(stream))
+    if rc:
+        raise MpfftError(rc, f"mpfft_stage({which})")
+
+
+def workspace_views(ws, n1, n2, depth, w):
+    """(digA, topA, digB, topB) views into a single-GPU workspace tensor (slot-major)."""
+    import torch
+    P = plan_info(n1, n2, depth, w)
+    slots, l = 2 * P["n"], P["l"]
+    dig = slots * l * 8
+    top = (slots * 4 + 255) // 256 * 256
+    u8 = ws.view(torch.uint8)
+    digA = u8[0:dig].view(torch.int64).view(slots, l)
+    topA = u8[dig:dig + slots * 4].view(torch.int32)
+    digB = u8[dig + top:2 * dig + top].view(torch.int64).view(slots, l)
+    topB = u8[2 * dig + top:2 * dig + top + slots * 4].view(torch.int32)
+    return digA, topA, digB, topB

@@ -1,0 +1,582 @@
+// mpfft.hip -- host orchestration and C ABI of the MI355X-native new_mpn_mul.
+//
+// The drop-in boundary is new_mpn_mul(r1, i1, n1, i2, n2, depth, w)
+// (/root/reference/mul_fft.c:3190-3191); see include/mpfft.h.  Everything below
+// the boundary is a re-design for gfx950:
+//
+//   1. forward column pass(es): split fused into the first pass; truncated DIF of
+//      length NR on every column, both operands in one launch        (a2-a12)
+//   2. forward row pass(es): MFA twiddle fused into the load, DIF of length NC
+//      over the T/NC live rows, canonical store                       (a3, a7)
+//   3. pointwise mulmod 2^N+1 over the T live slots                   (a20)
+//   4. inverse row pass(es), MFA un-twiddle fused into the store      (a13, a15)
+//   5. truncated inverse column transform (van der Hoeven), driven as a host
+//      recursion of block IFFT passes and element-wise pair steps     (a13, a14)
+//   6. scale by 2^-(depth+1) + canonicalise                           (a21)
+//   7. combine: limb-parallel shifted sums + device-wide carry scan   (a22)
+//
+// Slot layout: operand X lives in slots 0..2n-1 (row-major, NC columns).  After
+// stage 2, slot p*NC + q holds X_{revbin(p) + NR*revbin(q)} (the reference's
+// slot map, mul_fft.c:2357, up to its two revbin permutations, which we never
+// perform because the inverse undoes them).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <mutex>
+
+typedef uint8_t u8;
+#include "kernels.hpp"
+#include "../../include/mpfft.h"
+
+// ---------------------------------------------------------------------------
+// parameters (mul_fft.c:3193-3203)
+// ---------------------------------------------------------------------------
+struct Plan {
+    long n1, n2;
+    int depth;
+    long w;
+    long n, l;
+    u64 N, bits1;
+    long NC, NR;
+    int lbC, lbR;
+    long j1, j2, trunc, Tr, len, total;
+    int U, tpb, maxlogg;
+    size_t slots;       // allocated slots per operand
+    size_t off_digA, off_topA, off_digB, off_topB, off_lo, off_hi, off_bg, off_bp, off_bc, bytes;
+    long nblk;
+};
+
+static int ilog2(long v) { int d = 0; while ((1L << d) < v) ++d; return d; }
+
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned long w)
+{
+    memset(p, 0, sizeof(*p));
+    if (n1 < 1 || n2 < 1) return MPFFT_EINVAL;
+    if (depth < 2 || depth > 30 || w < 1 || w > 4096) return MPFFT_EINVAL;
+    p->n1 = n1;
+    p->n2 = n2;
+    p->depth = (int)depth;
+    p->w = (long)w;
+    p->n = 1L << depth;
+    if (((u64)p->n * w) % 64) return MPFFT_EINVAL;          // N must be a whole number of limbs
+    p->N = (u64)p->n * w;
+    p->l = (long)(p->N / 64);
+    if (p->N <= depth) return MPFFT_EINVAL;
+    p->bits1 = (p->N - depth) / 2;
+    if (p->bits1 < 1) return MPFFT_EINVAL;
+    p->NC = 1L << (depth / 2);
+    p->NR = 2 * p->n / p->NC;
+    p->lbC = ilog2(p->NC);
+    p->lbR = ilog2(p->NR);
+    p->j1 = (long)((64 * (u64)n1 - 1) / p->bits1 + 1);
+    p->j2 = (long)((64 * (u64)n2 - 1) / p->bits1 + 1);
+    p->len = p->j1 + p->j2 - 1;
+    if (p->len > 2 * p->n) return MPFFT_ETOOBIG;             // product does not fit the convolution
+    p->trunc = ((p->j1 + p->j2 - 2 + 2 * p->NC) / (2 * p->NC)) * 2 * p->NC;
+    p->Tr = p->trunc / p->NC;
+    p->total = n1 + n2;
+    if (p->l > 4096) return MPFFT_EUNSUPPORTED;              // pointwise LDS budget (24 l bytes)
+    long tpb = 64;
+    while (tpb < p->l && tpb < 1024) tpb *= 2;
+    long U = (p->l + tpb - 1) / tpb;
+    int Up = 1;
+    while (Up < U) Up *= 2;
+    p->tpb = (int)tpb;
+    p->U = Up;
+    p->maxlogg = Up == 1 ? 4 : Up == 2 ? 3 : Up == 4 ? 2 : 1;
+    p->slots = (size_t)2 * p->n;
+    size_t o = 0;
+    const size_t dig = p->slots * p->l * 8, top = align_up(p->slots * 4, 256);
+    p->off_digA = o; o += dig;
+    p->off_topA = o; o += top;
+    p->off_digB = o; o += dig;
+    p->off_topB = o; o += top;
+    p->off_lo = o; o += align_up((size_t)p->total * 8, 256);
+    p->off_hi = o; o += align_up((size_t)p->total * 4, 256);
+    p->nblk = (p->total + 256 * CARRY_V - 1) / (256 * CARRY_V);
+    p->off_bg = o; o += align_up((size_t)p->nblk, 256);
+    p->off_bp = o; o += align_up((size_t)p->nblk, 256);
+    p->off_bc = o; o += align_up((size_t)p->nblk, 256);
+    p->bytes = o;
+    return MPFFT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// kernel dispatch
+// ---------------------------------------------------------------------------
+typedef void (*pass_fn)(PassArgs);
+
+template <int U>
+static pass_fn pick_pass(int logg, int dir)
+{
+    constexpr int ML = U == 1 ? 4 : U == 2 ? 3 : U == 4 ? 2 : 1;
+    if (dir == 0) {
+        switch (logg) {
+        case 1: return k_pass<U, 1, 0>;
+        case 2: if (ML >= 2) return k_pass<U, (ML >= 2 ? 2 : 1), 0>; break;
+        case 3: if (ML >= 3) return k_pass<U, (ML >= 3 ? 3 : 1), 0>; break;
+        case 4: if (ML >= 4) return k_pass<U, (ML >= 4 ? 4 : 1), 0>; break;
+        }
+    } else {
+        switch (logg) {
+        case 1: return k_pass<U, 1, 1>;
+        case 2: if (ML >= 2) return k_pass<U, (ML >= 2 ? 2 : 1), 1>; break;
+        case 3: if (ML >= 3) return k_pass<U, (ML >= 3 ? 3 : 1), 1>; break;
+        case 4: if (ML >= 4) return k_pass<U, (ML >= 4 ? 4 : 1), 1>; break;
+        }
+    }
+    return nullptr;
+}
+
+static pass_fn get_pass(int U, int logg, int dir)
+{
+    switch (U) {
+    case 1: return pick_pass<1>(logg, dir);
+    case 2: return pick_pass<2>(logg, dir);
+    case 4: return pick_pass<4>(logg, dir);
+    }
+    return nullptr;
+}
+
+// dynamic LDS above 64 KiB must be opted into per kernel (gfx950 has 160 KiB per CU)
+static void allow_lds(const void *f, size_t bytes)
+{
+    if (bytes > 64 * 1024) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+#define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { last_hip_error = e_; return MPFFT_EHIP; } } while (0)
+static thread_local hipError_t last_hip_error = hipSuccess;
+
+struct Exec {
+    const Plan &P;
+    hipStream_t s;
+    u64 *digA, *digB;
+    int *topA, *topB;
+    int nbuf;
+    size_t lds_pass;
+    Exec(const Plan &p, hipStream_t st, unsigned char *ws) : P(p), s(st)
+    {
+        digA = (u64 *)(ws + P.off_digA);
+        topA = (int *)(ws + P.off_topA);
+        digB = (u64 *)(ws + P.off_digB);
+        topB = (int *)(ws + P.off_topB);
+        const size_t one = (size_t)2 * P.l * sizeof(i64);
+        nbuf = (2 * one <= 64 * 1024) ? 2 : 1;
+        lds_pass = nbuf * one + (3 * P.U * 16 + 8) * sizeof(u64);
+    }
+
+    int pass(PassArgs a, int logg, int dir, int nops)
+    {
+        pass_fn f = get_pass(P.U, logg, dir);
+        if (!f) return MPFFT_EUNSUPPORTED;
+        allow_lds((const void *)f, lds_pass);
+        a.nbuf = nbuf;
+        a.ngroups = 1 << (a.lbM - logg);
+        dim3 grid((unsigned)((long)a.nsub * a.ngroups), (unsigned)nops);
+        hipLaunchKernelGGL(f, grid, dim3(P.tpb), lds_pass, s, a);
+        HIPCHK(hipGetLastError());
+        return MPFFT_OK;
+    }
+
+    PassArgs base_args() const
+    {
+        PassArgs a;
+        memset(&a, 0, sizeof(a));
+        a.dig[0] = digA; a.dig[1] = digB;
+        a.top[0] = topA; a.top[1] = topB;
+        a.bits1 = P.bits1;
+        a.N = P.N;
+        a.l = (int)P.l;
+        return a;
+    }
+
+    // stage 1: split + forward truncated column DIF (length NR, root 2^(w NC))
+    int fwd_columns(const u64 *srcA, long nA, const u64 *srcB, long nB, int nops)
+    {
+        int lvl = 0;
+        while (lvl < P.lbR) {
+            int k = P.lbR - lvl < P.maxlogg ? P.lbR - lvl : P.maxlogg;
+            PassArgs a = base_args();
+            if (lvl == 0) {
+                a.src[0] = srcA; a.nsrc[0] = nA;
+                a.src[1] = srcB; a.nsrc[1] = nB;
+                a.zero_from = (int)P.Tr;
+            } else {
+                a.zero_from = (int)P.NR;
+            }
+            a.lbM = P.lbR;
+            a.lvl0 = lvl;
+            a.rho = (u64)P.w * P.NC;
+            a.sub_stride = 1;
+            a.pos_stride = P.NC;
+            a.nsub = (int)P.NC;
+            a.need = (int)P.Tr;
+            int rc = pass(a, k, 0, nops);
+            if (rc) return rc;
+            lvl += k;
+        }
+        return MPFFT_OK;
+    }
+
+    // stage 2: MFA twiddle + row DIF (length NC, root 2^(w NR)), canonical out
+    int fwd_rows(int nops)
+    {
+        int lvl = 0;
+        while (lvl < P.lbC) {
+            int k = P.lbC - lvl < P.maxlogg ? P.lbC - lvl : P.maxlogg;
+            PassArgs a = base_args();
+            a.lbM = P.lbC;
+            a.lvl0 = lvl;
+            a.rho = (u64)P.w * P.NR;
+            a.sub_stride = P.NC;
+            a.pos_stride = 1;
+            a.nsub = (int)P.Tr;
+            a.zero_from = (int)P.NC;
+            a.need = (int)P.NC;
+            if (lvl == 0) { a.tw_mode = 1; a.tw_w = (u64)P.w; a.tw_lbR = P.lbR; }
+            if (lvl + k == P.lbC) a.canon = 1;
+            int rc = pass(a, k, 0, nops);
+            if (rc) return rc;
+            lvl += k;
+        }
+        return MPFFT_OK;
+    }
+
+    int pointwise()
+    {
+        const size_t lds = (size_t)3 * 2 * P.l * 4 + (3 * P.U * 16 + 8) * 8;
+        void (*f)(u64 *, int *, const u64 *, const int *, int, u64) = nullptr;
+        switch (P.U) {
+        case 1: f = k_pointwise<1>; break;
+        case 2: f = k_pointwise<2>; break;
+        case 4: f = k_pointwise<4>; break;
+        }
+        allow_lds((const void *)f, lds);
+        hipLaunchKernelGGL(f, dim3((unsigned)P.trunc), dim3(P.tpb), lds, s, digA, topA, (const u64 *)digB,
+                           (const int *)topB, (int)P.l, P.N);
+        HIPCHK(hipGetLastError());
+        return MPFFT_OK;
+    }
+
+    // stage 4: row DIT inverse, MFA un-twiddle at the end
+    int inv_rows()
+    {
+        int hi = P.lbC;
+        while (hi > 0) {
+            int k = hi < P.maxlogg ? hi : P.maxlogg;
+            PassArgs a = base_args();
+            a.lbM = P.lbC;
+            a.lvl0 = hi - k;
+            a.rho = (u64)P.w * P.NR;
+            a.sub_stride = P.NC;
+            a.pos_stride = 1;
+            a.nsub = (int)P.Tr;
+            a.zero_from = (int)P.NC;
+            a.need = (int)P.NC;
+            if (hi - k == 0) { a.tw_mode = 2; a.tw_w = (u64)P.w; a.tw_lbR = P.lbR; }
+            int rc = pass(a, k, 1, 1);
+            if (rc) return rc;
+            hi -= k;
+        }
+        return MPFFT_OK;
+    }
+
+    // full inverse (DIT) over block [off, off + m) of every column
+    int ifft_block(long off, long m)
+    {
+        const int lbM = ilog2(m);
+        int hi = lbM;
+        while (hi > 0) {
+            int k = hi < P.maxlogg ? hi : P.maxlogg;
+            PassArgs a = base_args();
+            a.lbM = lbM;
+            a.lvl0 = hi - k;
+            a.rho = (u64)P.w * P.NC * (u64)(P.NR / m);
+            a.sub_stride = 1;
+            a.pos_stride = P.NC;
+            a.nsub = (int)P.NC;
+            a.pos_off = (int)off;
+            a.zero_from = (int)m;
+            a.need = (int)m;
+            int rc = pass(a, k, 1, 1);
+            if (rc) return rc;
+            hi -= k;
+        }
+        return MPFFT_OK;
+    }
+
+    int pairop(int op, long off, long h, long i0, long cnt, u64 rho)
+    {
+        if (cnt <= 0) return MPFFT_OK;
+        PairArgs a;
+        a.dig = digA;
+        a.top = topA;
+        a.N = P.N;
+        a.l = (int)P.l;
+        a.op = op;
+        a.NC = P.NC;
+        a.ncol = (int)P.NC;
+        a.off = (int)off;
+        a.h = (int)h;
+        a.i0 = (int)i0;
+        a.cnt = (int)cnt;
+        a.rho = rho;
+        const size_t lds = (size_t)2 * P.l * sizeof(i64) + (3 * P.U * 16 + 8) * sizeof(u64);
+        void (*f)(PairArgs) = nullptr;
+        switch (P.U) {
+        case 1: f = k_pairop<1>; break;
+        case 2: f = k_pairop<2>; break;
+        case 4: f = k_pairop<4>; break;
+        }
+        allow_lds((const void *)f, lds);
+        hipLaunchKernelGGL(f, dim3((unsigned)(cnt * P.NC)), dim3(P.tpb), lds, s, a);
+        HIPCHK(hipGetLastError());
+        return MPFFT_OK;
+    }
+
+    u64 rho_blk(long m) const { return (u64)P.w * P.NC * (u64)(P.NR / m); }
+
+    // IFFT_radix2_truncate(_twiddle) (mul_fft.c:1733-1790): outputs [off, off+t) known,
+    // inputs >= t zero; root of a length-m block = 2^(w NC NR/m)
+    int itft(long off, long m, long t)
+    {
+        int rc;
+        const long h = m / 2;
+        if (t == m) return ifft_block(off, m);
+        if (t <= h) {
+            if ((rc = itft(off, h, t))) return rc;
+            return pairop(OP_DOUBLE, off, h, 0, t, 0);
+        }
+        if ((rc = ifft_block(off, h))) return rc;
+        if ((rc = pairop(OP_FILL, off, h, t - h, h - (t - h), rho_blk(m)))) return rc;
+        if ((rc = itft1(off + h, h, t - h))) return rc;
+        if ((rc = pairop(OP_IBFLY, off, h, 0, t - h, rho_blk(m)))) return rc;
+        return pairop(OP_DOUBLE, off, h, t - h, h - (t - h), 0);
+    }
+
+    // IFFT_radix2_truncate1(_twiddle) (mul_fft.c:1604-1668): inputs [t, m) known
+    int itft1(long off, long m, long t)
+    {
+        int rc;
+        const long h = m / 2;
+        if (t == m) return ifft_block(off, m);
+        if (t <= h) {
+            if ((rc = pairop(OP_HALFADD, off, h, t, h - t, 0))) return rc;
+            if ((rc = itft1(off, h, t))) return rc;
+            return pairop(OP_TWOXMY, off, h, 0, t, 0);
+        }
+        if ((rc = ifft_block(off, h))) return rc;
+        if ((rc = pairop(OP_FIX, off, h, t - h, h - (t - h), rho_blk(m)))) return rc;
+        if ((rc = itft1(off + h, h, t - h))) return rc;
+        return pairop(OP_IBFLY, off, h, 0, t - h, rho_blk(m));
+    }
+
+    int scale()
+    {
+        const size_t lds = (size_t)2 * P.l * sizeof(i64) + (3 * P.U * 16 + 8) * sizeof(u64);
+        void (*f)(u64 *, int *, int, u64, u64) = nullptr;
+        switch (P.U) {
+        case 1: f = k_scale<1>; break;
+        case 2: f = k_scale<2>; break;
+        case 4: f = k_scale<4>; break;
+        }
+        const u64 e = 2 * P.N - (u64)(P.depth + 1);
+        allow_lds((const void *)f, lds);
+        hipLaunchKernelGGL(f, dim3((unsigned)P.trunc), dim3(P.tpb), lds, s, digA, topA, (int)P.l, P.N, e);
+        HIPCHK(hipGetLastError());
+        return MPFFT_OK;
+    }
+
+    int combine(u64 *r, unsigned char *ws)
+    {
+        u64 *lo = (u64 *)(ws + P.off_lo);
+        u32 *hi = (u32 *)(ws + P.off_hi);
+        u8 *bg = ws + P.off_bg, *bp = ws + P.off_bp, *bc = ws + P.off_bc;
+        hipLaunchKernelGGL(k_comb_sum, dim3((unsigned)((P.total + 255) / 256)), dim3(256), 0, s,
+                           (const u64 *)digA, (int)P.l, P.N, P.bits1, P.len, P.total, lo, hi);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_carry_blocks, dim3((unsigned)P.nblk), dim3(256), 0, s, (const u64 *)lo,
+                           (const u32 *)hi, P.total, bg, bp);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_carry_scan, dim3(1), dim3(1024), 0, s, (const u8 *)bg, (const u8 *)bp, P.nblk, bc);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_carry_apply, dim3((unsigned)P.nblk), dim3(256), 0, s, (const u64 *)lo,
+                           (const u32 *)hi, P.total, (const u8 *)bc, r);
+        HIPCHK(hipGetLastError());
+        return MPFFT_OK;
+    }
+};
+
+static int run_all(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, unsigned char *ws, hipStream_t s)
+{
+    Exec X(P, s, ws);
+    int rc;
+    if ((rc = X.fwd_columns(d_i1, P.n1, d_i2, P.n2, 2))) return rc;
+    if ((rc = X.fwd_rows(2))) return rc;
+    if ((rc = X.pointwise())) return rc;
+    if ((rc = X.inv_rows())) return rc;
+    if ((rc = X.itft(0, P.NR, P.Tr))) return rc;
+    if ((rc = X.scale())) return rc;
+    return X.combine(d_r, ws);
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+const char *mpfft_strerror(int code)
+{
+    switch (code) {
+    case MPFFT_OK: return "ok";
+    case MPFFT_EINVAL: return "invalid parameters (need n1,n2 >= 1, 2 <= depth <= 30, n*w % 64 == 0)";
+    case MPFFT_ETOOBIG: return "operands too large for the convolution: need j1 + j2 - 1 <= 2^(depth+1)";
+    case MPFFT_EUNSUPPORTED: return "coefficient size n*w/64 > 4096 limbs is not supported";
+    case MPFFT_ENOMEM: return "device allocation failed";
+    case MPFFT_EHIP: return hipGetErrorString(last_hip_error);
+    case MPFFT_ENODEV: return "no HIP device";
+    }
+    return "unknown error";
+}
+
+int mpfft_version(void) { return MPFFT_VERSION; }
+
+int mpfft_check_params(long n1, long n2, unsigned long depth, unsigned long w)
+{
+    Plan P;
+    return make_plan(&P, n1, n2, depth, w);
+}
+
+size_t mpfft_workspace_bytes(long n1, long n2, unsigned long depth, unsigned long w)
+{
+    Plan P;
+    if (make_plan(&P, n1, n2, depth, w)) return 0;
+    return P.bytes;
+}
+
+int mpfft_plan_info(long n1, long n2, unsigned long depth, unsigned long w, long *out)
+{
+    Plan P;
+    int rc = make_plan(&P, n1, n2, depth, w);
+    if (rc) return rc;
+    out[0] = P.n; out[1] = P.l; out[2] = P.NC; out[3] = P.j1; out[4] = P.j2;
+    out[5] = P.trunc; out[6] = (long)P.bits1; out[7] = P.NR; out[8] = P.tpb; out[9] = P.U;
+    return MPFFT_OK;
+}
+
+int mpfft_mul_device(uint64_t *d_r, const uint64_t *d_i1, long n1, const uint64_t *d_i2, long n2,
+                     unsigned long depth, unsigned long w, void *d_ws, size_t ws_bytes, void *stream)
+{
+    Plan P;
+    int rc = make_plan(&P, n1, n2, depth, w);
+    if (rc) return rc;
+    if (!d_ws || ws_bytes < P.bytes) return MPFFT_ENOMEM;
+    (void)hipGetLastError();  // clear a sticky error left by another library in this process
+    return run_all(P, d_r, d_i1, d_i2, (unsigned char *)d_ws, (hipStream_t)stream);
+}
+
+// stage entry points (device pointers), used by the stage-parity tests and the
+// multi-GPU driver.  `ws` has the single-GPU workspace layout for (n1, n2, depth, w).
+int mpfft_stage(int stage, const uint64_t *d_i1, const uint64_t *d_i2, uint64_t *d_r, long n1, long n2,
+                unsigned long depth, unsigned long w, void *d_ws, size_t ws_bytes, void *stream)
+{
+    Plan P;
+    int rc = make_plan(&P, n1, n2, depth, w);
+    if (rc) return rc;
+    if (!d_ws || ws_bytes < P.bytes) return MPFFT_ENOMEM;
+    (void)hipGetLastError();
+    Exec X(P, (hipStream_t)stream, (unsigned char *)d_ws);
+    switch (stage) {
+    case MPFFT_STAGE_FWD_COLUMNS: return X.fwd_columns(d_i1, n1, d_i2, n2, 2);
+    case MPFFT_STAGE_FWD_ROWS: return X.fwd_rows(2);
+    case MPFFT_STAGE_POINTWISE: return X.pointwise();
+    case MPFFT_STAGE_INV_ROWS: return X.inv_rows();
+    case MPFFT_STAGE_INV_COLUMNS: return X.itft(0, P.NR, P.Tr);
+    case MPFFT_STAGE_SCALE: return X.scale();
+    case MPFFT_STAGE_COMBINE: return X.combine(d_r, (unsigned char *)d_ws);
+    }
+    return MPFFT_EINVAL;
+}
+
+// host-pointer entry with status
+static std::mutex g_mu;
+static unsigned char *g_ws = nullptr;
+static size_t g_ws_bytes = 0;
+static u64 *g_io = nullptr;
+static size_t g_io_bytes = 0;
+static hipStream_t g_stream = nullptr;
+
+int mpfft_mul_ex(uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i2, long n2, unsigned long depth,
+                 unsigned long w)
+{
+    Plan P;
+    int rc = make_plan(&P, n1, n2, depth, w);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(g_mu);
+    (void)hipGetLastError();
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return MPFFT_ENODEV;
+    if (!g_stream) HIPCHK(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
+    if (g_ws_bytes < P.bytes) {
+        if (g_ws) (void)hipFree(g_ws);
+        g_ws = nullptr;
+        g_ws_bytes = 0;
+        if (hipMalloc((void **)&g_ws, P.bytes) != hipSuccess) return MPFFT_ENOMEM;
+        g_ws_bytes = P.bytes;
+    }
+    const size_t io = (size_t)2 * (n1 + n2) * 8;
+    if (g_io_bytes < io) {
+        if (g_io) (void)hipFree(g_io);
+        g_io = nullptr;
+        g_io_bytes = 0;
+        if (hipMalloc((void **)&g_io, io) != hipSuccess) return MPFFT_ENOMEM;
+        g_io_bytes = io;
+    }
+    u64 *d_i1 = g_io, *d_i2 = g_io + n1, *d_r = g_io + n1 + n2;
+    HIPCHK(hipMemcpyAsync(d_i1, i1, (size_t)n1 * 8, hipMemcpyHostToDevice, g_stream));
+    HIPCHK(hipMemcpyAsync(d_i2, i2, (size_t)n2 * 8, hipMemcpyHostToDevice, g_stream));
+    rc = run_all(P, d_r, d_i1, d_i2, g_ws, g_stream);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(r1, d_r, (size_t)(n1 + n2) * 8, hipMemcpyDeviceToHost, g_stream));
+    HIPCHK(hipStreamSynchronize(g_stream));
+    return MPFFT_OK;
+}
+
+// mul_fft.c:3190 -- same signature and meaning; fails loudly instead of segfaulting
+void new_mpn_mul(mp_limb_t *r1, mp_limb_t *i1, mp_size_t n1, mp_limb_t *i2, mp_size_t n2, mp_bitcnt_t depth,
+                 mp_bitcnt_t w)
+{
+    int rc = mpfft_mul_ex(r1, i1, n1, i2, n2, depth, w);
+    if (rc) {
+        fprintf(stderr, "new_mpn_mul(n1=%ld, n2=%ld, depth=%lu, w=%lu): %s\n", (long)n1, (long)n2,
+                (unsigned long)depth, (unsigned long)w, mpfft_strerror(rc));
+        abort();
+    }
+}
+
+// splitmix64-seeded xoshiro256** (BASELINE.md synthetic inputs; same stream as the oracle's)
+void mpfft_fill_random(uint64_t *buf, long cnt, uint64_t seed)
+{
+    uint64_t s[4], z = seed;
+    for (int i = 0; i < 4; i++) {
+        z += 0x9e3779b97f4a7c15ULL;
+        uint64_t x = z;
+        x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ULL;
+        x = (x ^ (x >> 27)) * 0x94d049bb133111ebULL;
+        s[i] = x ^ (x >> 31);
+    }
+    for (long i = 0; i < cnt; i++) {
+        const uint64_t r = s[1] * 5;
+        buf[i] = ((r << 7) | (r >> 57)) * 9;
+        const uint64_t t = s[1] << 17;
+        s[2] ^= s[0]; s[3] ^= s[1]; s[1] ^= s[2]; s[0] ^= s[3];
+        s[2] ^= t;
+        s[3] = (s[3] << 45) | (s[3] >> 19);
+    }
+}
+
+}  // extern "C"
