@@ -1,0 +1,173 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle and the
+exact product.  Bit-exact is the only bar (integer work).
+
+Covers: every stage against exact big-integer math (tests/gpu_stages.py), the
+reference-shaped new_mpn_mul over random and adversarial shapes (cf. the
+reference's integration tests test_mul4/test_mul5, mul_fft.c:5507-5608), the
+committed golden vectors, error behaviour, and the benchmark configs.
+"""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from helpers import max_limbs, to_int, valid_shape
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+STAGE_SHAPES = [(6, 1, 3, 2), (6, 1, 1, 1), (7, 1, 5, 4), (7, 3, 13, 2), (8, 2, 30, 25), (8, 4, 60, 50),
+                (9, 1, 30, 31), (10, 3, 300, 200), (11, 1, 1000, 1000), (5, 2, 2, 1), (4, 4, 1, 1),
+                (3, 8, 1, 1), (2, 16, 1, 1)]
+
+
+@pytest.mark.parametrize("depth,w,n1,n2", STAGE_SHAPES)
+def test_stages_exact(mp, torch_dev, depth, w, n1, n2):
+    from gpu_stages import run_stages
+    if not valid_shape(depth, w, n1, n2):
+        pytest.skip("shape does not fit")
+    a = mp.fill_random(n1, 1000 + depth * 7 + n1)
+    b = mp.fill_random(n2, 2000 + w * 3 + n2)
+    fails = run_stages(mp, depth, w, a, b, dev=torch_dev)
+    assert not fails, "\n".join(fails[:5])
+
+
+def _random_shapes(seed, per):
+    rng = random.Random(seed)
+    out = []
+    for depth in range(2, 14):
+        for w in (1, 2, 3, 4, 5, 8, 16, 32, 64):
+            if ((1 << depth) * w) % 64 or (1 << depth) * w // 64 > 4096:
+                continue
+            mx = max_limbs(depth, w)
+            if mx > 200000:
+                continue
+            out.append((depth, w, mx, mx))
+            for _ in range(per):
+                n1 = rng.randint(1, 2 * mx - 1)
+                n2 = rng.randint(1, max(1, 2 * mx - n1))
+                if valid_shape(depth, w, n1, n2):
+                    out.append((depth, w, n1, n2))
+    return out
+
+
+def test_new_mpn_mul_random_sweep(mp, oracle):
+    rng = random.Random(77)
+    shapes = _random_shapes(5, 2)
+    assert len(shapes) > 100
+    for depth, w, n1, n2 in shapes:
+        a = mp.fill_random(n1, rng.getrandbits(64))
+        b = mp.fill_random(n2, rng.getrandbits(64))
+        r = np.zeros(n1 + n2, dtype=np.uint64)
+        mp.new_mpn_mul(r, a, n1, b, n2, depth, w)
+        want = oracle.gmp_mul(a, b)
+        assert (r == want).all(), (depth, w, n1, n2)
+
+
+def test_adversarial_inputs(mp, oracle):
+    """all-ones (max carries), single bits, zeros, unbalanced, max size; values that
+    make transform coefficients hit 2^N (the pointwise c-flag, mul_fft.c:3250)."""
+    for depth, w in ((6, 1), (8, 2), (10, 1), (11, 8), (9, 64)):
+        mx = max_limbs(depth, w)
+        ones = np.full(mx, 2**64 - 1, dtype=np.uint64)
+        zero = np.zeros(mx, np.uint64)
+        bit = zero.copy()
+        bit[mx // 2] = 1 << 63
+        top1 = zero.copy()
+        top1[-1] = 1
+        alt = np.full(mx, 0xAAAAAAAAAAAAAAAA, np.uint64)
+        cases = [(ones, ones), (ones[:1], ones), (bit, ones), (zero, ones), (top1, top1), (alt, ones),
+                 (ones[: mx // 3], ones), (np.ones(1, np.uint64), ones)]
+        for a, b in cases:
+            if not valid_shape(depth, w, len(a), len(b)):
+                continue
+            got = mp.mul(a, b, depth, w)
+            assert (got == oracle.gmp_mul(a, b)).all(), (depth, w, len(a), len(b))
+
+
+def test_coefficient_equal_2N(mp, oracle):
+    """Operands whose transform has coefficients == 2^N == -1 mod p exercise the
+    top-limb-1 path of the pointwise product.  x_j = 2^bits1-1 pieces with the
+    all-ones operand hit it at small N; check many (depth, w) combinations."""
+    for depth, w in ((6, 1), (6, 2), (7, 1), (8, 1)):
+        mx = max_limbs(depth, w)
+        for fill in (0x8000000000000000, 0xFFFFFFFFFFFFFFFF, 1):
+            a = np.full(mx, fill, np.uint64)
+            for n1 in (1, 2, mx):
+                got = mp.mul(a[:n1], a, depth, w)
+                assert (got == oracle.gmp_mul(a[:n1], a)).all()
+
+
+def test_golden_vectors(mp):
+    path = os.path.join(GOLDEN, "products.json")
+    if not os.path.exists(path):
+        pytest.skip("no golden vectors")
+    with open(path) as f:
+        cases = json.load(f)
+    import hashlib
+    for c in cases:
+        a = mp.fill_random(c["n1"], int(c["seed1"], 16))
+        b = mp.fill_random(c["n2"], int(c["seed2"], 16))
+        got = mp.mul(a, b, c["depth"], c["w"])
+        if "product_hex" in c:
+            assert format(to_int(got), "x") == c["product_hex"], c["name"]
+        assert hashlib.sha256(got.tobytes()).hexdigest() == c["sha256"], c["name"]
+
+
+def test_errors_fail_loudly(mp):
+    a = np.ones(10, np.uint64)
+    with pytest.raises(mp.MpfftError):
+        mp.mul(a, a, 5, 3)            # n*w not a multiple of 64
+    big = np.ones(100000, np.uint64)
+    with pytest.raises(mp.MpfftError):
+        mp.mul(big, big, 6, 1)        # product does not fit
+    with pytest.raises(mp.MpfftError):
+        mp.mul(a, a, 1, 64)           # depth < 2
+
+
+def test_device_api_and_workspace_reuse(mp, oracle, torch_dev):
+    import torch
+    depth, w = 11, 8
+    for n1, n2 in ((261952, 261952), (1000, 250000), (5, 7)):
+        a = mp.fill_random(n1, 11)
+        b = mp.fill_random(n2, 12)
+        da = torch.from_numpy(a.view(np.int64)).to(torch_dev)
+        db = torch.from_numpy(b.view(np.int64)).to(torch_dev)
+        dr = torch.zeros(n1 + n2, dtype=torch.int64, device=torch_dev)
+        ws = mp.alloc_workspace(261952, 261952, depth, w, torch_dev)   # larger workspace is fine
+        ws.fill_(0x77)
+        for _ in range(2):                                            # reuse without re-zeroing
+            mp.mul_device(dr, da, n1, db, n2, depth, w, ws)
+        torch.cuda.synchronize()
+        assert (dr.cpu().numpy().view(np.uint64) == oracle.gmp_mul(a, b)).all()
+
+
+@pytest.mark.parametrize("cfg", ["C0", "C1"])
+def test_bench_configs_exact_vs_oracle(mp, oracle, cfg):
+    """C0/C1 at full size against the CPU restatement of the reference (bit-exact)."""
+    depth, w, nl = {"C0": (11, 1, 16384), "C1": (11, 8, 261952)}[cfg]
+    a = mp.fill_random(nl, 0x1001)
+    b = mp.fill_random(nl, 0x2002)
+    got = mp.mul(a, b, depth, w)
+    assert (got == oracle.new_mpn_mul(a, b, depth, w)).all()
+
+
+@pytest.mark.slow
+def test_c2_c3_exact_vs_gmp(mp, oracle):
+    """C2 (10^9-bit) and C3 (1.3x10^9-bit, odd trunc) against GMP mpn_mul."""
+    for depth, w, nl in ((15, 4, 15625000), (15, 4, 20312500)):
+        a = mp.fill_random(nl, 0x1001)
+        b = mp.fill_random(nl, 0x2002)
+        got = mp.mul(a, b, depth, w)
+        assert (got == oracle.gmp_mul(a, b)).all()

@@ -1,0 +1,77 @@
+"""CPU-only checks of the product library (no compute: this container has no GPU).
+
+- libmpfft.so loads and exports every function include/mpfft.h declares
+- parameter derivation equals the reference's (mul_fft.c:3193-3203, via the oracle)
+- invalid calls are rejected with a reason instead of the reference's segfault
+- with no GPU the compute entry points fail loudly (no CPU fallback exists)
+- the synthetic-input PRNG is the oracle's stream
+"""
+import os
+import random
+import re
+
+import numpy as np
+import pytest
+
+from helpers import valid_shape
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    src = open(os.path.join(ROOT, "include", "mpfft.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:void|int|size_t|const char \*)\s*\*?\s*(\w+)\s*\(", src, flags=re.M)))
+
+
+def test_exports_every_declared_symbol(mp):
+    names = declared_functions()
+    assert "new_mpn_mul" in names and "mpfft_mul_device" in names
+    lib = mp.lib()
+    for n in names:
+        assert hasattr(lib, n), n
+    assert lib.mpfft_version() >= 1
+
+
+def test_plan_matches_reference_parameters(mp, oracle):
+    rng = random.Random(3)
+    checked = 0
+    for _ in range(400):
+        depth = rng.randint(2, 17)
+        w = rng.choice([1, 2, 3, 4, 5, 8, 16, 64])
+        n1, n2 = rng.randint(1, 5000), rng.randint(1, 5000)
+        ok = ((1 << depth) * w) % 64 == 0 and valid_shape(depth, w, n1, n2) and (1 << depth) * w // 64 <= 4096
+        rc = mp.check_params(n1, n2, depth, w)
+        assert (rc == 0) == ok, (depth, w, n1, n2, rc)
+        if ok:
+            P = mp.plan_info(n1, n2, depth, w)
+            n, l, sq, j1, j2, trunc, bits1 = oracle.params(n1, n2, depth, w)
+            assert (P["n"], P["l"], P["NC"], P["j1"], P["j2"], P["trunc"], P["bits1"]) == \
+                (n, l, sq, j1, j2, trunc, bits1)
+            assert P["NR"] * P["NC"] == 2 * n
+            checked += 1
+    assert checked > 50
+
+
+def test_invalid_parameters_rejected(mp):
+    assert mp.check_params(10, 10, 5, 3) == 1          # n*w % 64
+    assert mp.check_params(0, 10, 8, 1) == 1
+    assert mp.check_params(10, 10, 1, 64) == 1         # depth < 2
+    assert mp.check_params(10**6, 10**6, 6, 1) == 2    # does not fit
+    assert mp.check_params(10, 10, 14, 64) == 3        # l > 4096
+    with pytest.raises(mp.MpfftError):
+        mp.plan_info(10, 10, 5, 3)
+
+
+def test_compute_fails_loudly_without_gpu(mp):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    a = np.ones(4, np.uint64)
+    with pytest.raises(mp.MpfftError):
+        mp.mul(a, a, 6, 1)
+
+
+def test_prng_matches_oracle(mp, oracle):
+    for seed in (0x1001, 0x2002, 7):
+        assert (mp.fill_random(1000, seed) == oracle.fill_random(1000, seed)).all()
