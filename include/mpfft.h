@@ -66,6 +66,10 @@ int mpfft_check_params(long n1, long n2, unsigned long depth, unsigned long w);
  * (mul_fft.c:3193-3203). */
 int mpfft_plan_info(long n1, long n2, unsigned long depth, unsigned long w, long *out);
 
+/* Byte offsets inside a single-GPU workspace (tests / multi-GPU driver):
+ * out[8] = digA, topA, cbA, digB, topB, cbB, slots per operand, carry-mask words per slot. */
+int mpfft_workspace_layout(long n1, long n2, unsigned long depth, unsigned long w, size_t *out);
+
 /* One stage of the pipeline on a single-GPU workspace (stage-parity tests, multi-GPU driver). */
 #define MPFFT_STAGE_FWD_COLUMNS 0   /* split + truncated column DIF, both operands   (mul_fft.c:2374-2390) */
 #define MPFFT_STAGE_FWD_ROWS 1      /* MFA twiddle + row DIF, canonical out           (mul_fft.c:2392-2408) */

@@ -66,6 +66,8 @@ def lib():
         h.mpfft_check_params.restype = ctypes.c_int
         h.mpfft_plan_info.argtypes = [_L, _L, _UL, _UL, ctypes.POINTER(ctypes.c_long)]
         h.mpfft_plan_info.restype = ctypes.c_int
+        h.mpfft_workspace_layout.argtypes = [_L, _L, _UL, _UL, ctypes.POINTER(ctypes.c_size_t)]
+        h.mpfft_workspace_layout.restype = ctypes.c_int
         h.mpfft_strerror.argtypes = [ctypes.c_int]
         h.mpfft_strerror.restype = ctypes.c_char_p
         h.mpfft_version.argtypes = []
@@ -163,16 +165,27 @@ def stage(which, d_i1, d_i2, d_r, n1, n2, depth, w, ws, stream=None):
         raise MpfftError(rc, f"mpfft_stage({which})")
 
 
+def workspace_layout(n1, n2, depth, w):
+    out = (ctypes.c_size_t * 8)()
+    rc = lib().mpfft_workspace_layout(n1, n2, depth, w, out)
+    if rc:
+        raise MpfftError(rc, "workspace_layout")
+    keys = ("digA", "topA", "cbA", "digB", "topB", "cbB", "slots", "cbw")
+    return dict(zip(keys, list(out)))
+
+
 def workspace_views(ws, n1, n2, depth, w):
-    """(digA, topA, digB, topB) views into a single-GPU workspace tensor (slot-major)."""
+    """(digA, topA, digB, topB) views into a single-GPU workspace tensor (slot-major).
+    Only meaningful for canonically stored stages (carry masks zero)."""
     import torch
     P = plan_info(n1, n2, depth, w)
-    slots, l = 2 * P["n"], P["l"]
-    dig = slots * l * 8
-    top = (slots * 4 + 255) // 256 * 256
+    lay = workspace_layout(n1, n2, depth, w)
+    slots, l = lay["slots"], P["l"]
     u8 = ws.view(torch.uint8)
-    digA = u8[0:dig].view(torch.int64).view(slots, l)
-    topA = u8[dig:dig + slots * 4].view(torch.int32)
-    digB = u8[dig + top:2 * dig + top].view(torch.int64).view(slots, l)
-    topB = u8[2 * dig + top:2 * dig + top + slots * 4].view(torch.int32)
-    return digA, topA, digB, topB
+
+    def dig(off):
+        return u8[off:off + slots * l * 8].view(torch.int64).view(slots, l)
+
+    def top(off):
+        return u8[off:off + slots * 4].view(torch.int32)
+    return dig(lay["digA"]), top(lay["topA"]), dig(lay["digB"]), top(lay["topB"])

@@ -24,6 +24,7 @@
 
 struct PassArgs {
     u64 *dig[2];
+    u64 *cb[2];
     int *top[2];
     const u64 *src[2];   // non-null: load coefficients straight from the operand (fused split)
     long nsrc[2];
@@ -44,48 +45,85 @@ struct PassArgs {
     int nbuf;            // LDS staging buffers (1 or 2)
 };
 
-// LDS carve: [stage0: 2l i64][stage1: 2l i64 if nbuf == 2][scan scratch]
-__device__ __forceinline__ u64 *scan_scratch(unsigned char *smem, int l, int nbuf)
-{
-    return (u64 *)(smem + (size_t)nbuf * 2 * l * sizeof(i64));
-}
-
-template <int U>
-struct Rotor {
-    const WG &c;
-    i64 *st0, *st1;
-    int nbuf, l;
-    u64 N;
-    int rc;
-    __device__ Rotor(const WG &c_, i64 *s0, i64 *s1, int nb, int l_, u64 N_)
-        : c(c_), st0(s0), st1(s1), nbuf(nb), l(l_), N(N_), rc(0) {}
-    // x <- x * 2^e mod p.  e must be workgroup-uniform.
-    __device__ __forceinline__ void operator()(i64 (&x)[2 * U], u64 e)
-    {
-        const Rot r = make_rot(e, N);
-        i64 *st = (nbuf > 1 && (rc & 1)) ? st1 : st0;
-        ++rc;
-        rot_write<U>(c, x, st, l);
-        __syncthreads();
-        rot_read<U>(c, x, st, r, l);
-        if (nbuf == 1) __syncthreads();
-    }
-    __device__ __forceinline__ void drain() { if (nbuf > 1) __syncthreads(); }
+// LDS carve for the coefficient kernels:
+//   [stage: rb * 2l i64][edge: norm_edge_ints int32][scan scratch: norm_scr_u64 u64]
+struct Lds {
+    i64 *stage;
+    int *edge;
+    u64 *scr;
 };
 
+__host__ __device__ inline size_t lds_bytes(int l, int rb, int G, int U, int nw)
+{
+    size_t st = (size_t)rb * 2 * l * sizeof(i64);
+    size_t ed = ((size_t)norm_edge_ints(G, U, nw) * sizeof(int) + 15) / 16 * 16;
+    return st + ed + (size_t)norm_scr_u64(G, U, nw) * sizeof(u64);
+}
+
+template <int U, int G>
+__device__ __forceinline__ Lds lds_carve(unsigned char *smem, int l, int rb, int nw)
+{
+    Lds d;
+    d.stage = (i64 *)smem;
+    unsigned char *p = smem + (size_t)rb * 2 * l * sizeof(i64);
+    d.edge = (int *)p;
+    p += ((size_t)norm_edge_ints(G, U, nw) * sizeof(int) + 15) / 16 * 16;
+    d.scr = (u64 *)p;
+    return d;
+}
+
+// Multiply x[i] by 2^ee[i] (mod p) for every i with ee[i] != 0.  The rotations are
+// staged rb coefficients at a time through LDS: two barriers per batch.
+template <int U, int G>
+__device__ __forceinline__ void rotate_set(const WG &c, i64 (&x)[G][2 * U], const u64 (&ee)[G], u64 N, int l,
+                                           i64 *stage, int rb)
+{
+    int slot[G];
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < G; ++i) slot[i] = ee[i] ? cnt++ : -1;
+    for (int b0 = 0; b0 < cnt; b0 += rb) {
+#pragma unroll
+        for (int i = 0; i < G; ++i)
+            if (slot[i] >= b0 && slot[i] < b0 + rb) rot_write<U>(c, x[i], stage + (size_t)(slot[i] - b0) * 2 * l, l);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < G; ++i)
+            if (slot[i] >= b0 && slot[i] < b0 + rb)
+                rot_read<U>(c, x[i], stage + (size_t)(slot[i] - b0) * 2 * l, make_rot(ee[i], N), l);
+        __syncthreads();
+    }
+}
+
+template <int U, int G>
+__device__ __forceinline__ void normalize_store(const WG &c, const i64 (&x)[G][2 * U], const long (&slot)[G],
+                                                const bool (&keep)[G], bool canon, const Coef &st, int l,
+                                                const Lds &sm)
+{
+    u64 y[G][U];
+    int tv[G], cy[G][U];
+    wg_norm_multi<U, G>(c, x, y, tv, cy, l, canon, sm.edge, sm.scr);
+#pragma unroll
+    for (int i = 0; i < G; ++i)
+        if (keep[i]) store_coeff<U>(c, y[i], cy[i], tv[i], st, slot[i], l);
+}
+
+// U == 1 kernels run with <= 256 threads (l <= 256 limbs): let them use up to 256 VGPRs
+#define MPF_LB(U) ((U) == 1 ? 256 : 1024)
+
 template <int U, int LOGG, int DIR>
-__global__ __launch_bounds__(1024) void k_pass(PassArgs a)
+__global__ __launch_bounds__(MPF_LB(U)) void k_pass(PassArgs a)
 {
     constexpr int G = 1 << LOGG;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const WG c = wg_ctx();
     const int l = a.l;
-    i64 *st0 = (i64 *)smem;
-    i64 *st1 = st0 + 2 * l;
-    u64 *scr = scan_scratch(smem, l, a.nbuf);
+    const Lds sm = lds_carve<U, G>(smem, l, a.nbuf, c.nw);
     const int op = blockIdx.y;
-    u64 *dig = a.dig[op];
-    int *top = a.top[op];
+    Coef st;
+    st.dig = a.dig[op];
+    st.cb = a.cb[op];
+    st.top = a.top[op];
     const int sub = (int)(blockIdx.x / a.ngroups);
     const int grp = (int)(blockIdx.x % a.ngroups);
     const int lobits = a.lbM - a.lvl0 - LOGG;
@@ -109,17 +147,15 @@ __global__ __launch_bounds__(1024) void k_pass(PassArgs a)
     for (int i = 0; i < G; ++i) {
         if (DIR == 0 && pos[i] >= a.zero_from) zero_coeff<U>(x[i]);
         else if (a.src[op]) load_split<U>(c, x[i], a.src[op], a.nsrc[op], slot[i], a.bits1, l);
-        else load_coeff<U>(c, x[i], dig, top, slot[i], l);
+        else load_coeff<U>(c, x[i], st, slot[i], l);
     }
 
-    Rotor<U> rot(c, st0, st1, a.nbuf, l, a.N);
     const long rsub = (a.tw_mode) ? revbin_dev(sub, a.tw_lbR) : 0;
-    if (a.tw_mode == 1) {
+    u64 ee[G];
+    if (a.tw_mode == 1) {  // MFA twiddle 2^(w * c * revbin(row)) (README:74-91)
 #pragma unroll
-        for (int i = 0; i < G; ++i) {
-            u64 e = (a.tw_w * (u64)(a.pos_off + pos[i]) * (u64)rsub) % N2;
-            if (e) rot(x[i], e);
-        }
+        for (int i = 0; i < G; ++i) ee[i] = (u32)(a.tw_w * (u64)(a.pos_off + pos[i]) * (u64)rsub) % (u32)N2;
+        rotate_set<U, G>(c, x, ee, a.N, l, sm.stage, a.nbuf);
     }
 
 #pragma unroll
@@ -127,12 +163,14 @@ __global__ __launch_bounds__(1024) void k_pass(PassArgs a)
         const int level = DIR == 0 ? a.lvl0 + li : a.lvl0 + LOGG - 1 - li;
         const int jb = DIR == 0 ? LOGG - 1 - li : li;
         const int h = 1 << (a.lbM - level - 1);
-        const u64 unit = (a.rho << level) % N2;
+        const u32 unit = (u32)(a.rho << level) % (u32)N2;
+#pragma unroll
+        for (int i = 0; i < G; ++i) ee[i] = 0;
 #pragma unroll
         for (int i = 0; i < G; ++i) {
             if ((i >> jb) & 1) continue;
             const int k = i | (1 << jb);
-            const u64 e = ((u64)(pos[i] & (h - 1)) * unit) % N2;
+            const u64 e = ((u32)(pos[i] & (h - 1)) * unit) % (u32)N2;
             if (DIR == 0) {
 #pragma unroll
                 for (int q = 0; q < 2 * U; ++q) {
@@ -140,9 +178,17 @@ __global__ __launch_bounds__(1024) void k_pass(PassArgs a)
                     x[i][q] = s;
                     x[k][q] = d;
                 }
-                if (e) rot(x[k], e);
+                ee[k] = e;
             } else {
-                if (e) rot(x[k], N2 - e);
+                ee[k] = e ? N2 - e : 0;
+            }
+        }
+        rotate_set<U, G>(c, x, ee, a.N, l, sm.stage, a.nbuf);
+        if (DIR == 1) {
+#pragma unroll
+            for (int i = 0; i < G; ++i) {
+                if ((i >> jb) & 1) continue;
+                const int k = i | (1 << jb);
 #pragma unroll
                 for (int q = 0; q < 2 * U; ++q) {
                     const i64 s = x[i][q] + x[k][q], d = x[i][q] - x[k][q];
@@ -153,25 +199,19 @@ __global__ __launch_bounds__(1024) void k_pass(PassArgs a)
         }
     }
 
-    if (a.tw_mode == 2) {
+    if (a.tw_mode == 2) {  // inverse MFA twiddle
 #pragma unroll
         for (int i = 0; i < G; ++i) {
-            u64 e = (a.tw_w * (u64)(a.pos_off + pos[i]) * (u64)rsub) % N2;
-            if (e) rot(x[i], N2 - e);
+            const u64 e = (u32)(a.tw_w * (u64)(a.pos_off + pos[i]) * (u64)rsub) % (u32)N2;
+            ee[i] = e ? N2 - e : 0;
         }
+        rotate_set<U, G>(c, x, ee, a.N, l, sm.stage, a.nbuf);
     }
-    __syncthreads();
 
+    bool keep[G];
 #pragma unroll
-    for (int i = 0; i < G; ++i) {
-        if (DIR == 0) {
-            const int fstart = pos[i] & ~((1 << lobits) - 1);
-            if (fstart >= a.need) continue;
-        }
-        u64 y[U];
-        const int tv = wg_normalize<U>(c, x[i], y, l, a.canon != 0, st0, scr);
-        store_coeff<U>(c, y, tv, dig, top, slot[i], l);
-    }
+    for (int i = 0; i < G; ++i) keep[i] = DIR == 1 || (pos[i] & ~((1 << lobits) - 1)) < a.need;
+    normalize_store<U, G>(c, x, slot, keep, a.canon != 0, st, l, sm);
 }
 
 // --------------------------------------------------------------------------
@@ -181,6 +221,7 @@ enum { OP_DOUBLE = 0, OP_HALFADD = 1, OP_FILL = 2, OP_FIX = 3, OP_TWOXMY = 4, OP
 
 struct PairArgs {
     u64 *dig;
+    u64 *cb;
     int *top;
     u64 N;
     int l;
@@ -197,95 +238,93 @@ __global__ __launch_bounds__(1024) void k_pairop(PairArgs a)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const WG c = wg_ctx();
     const int l = a.l;
-    i64 *st = (i64 *)smem;
-    u64 *scr = scan_scratch(smem, l, 1);
+    const Lds sm = lds_carve<U, 2>(smem, l, 2, c.nw);
     const int col = (int)(blockIdx.x % a.ncol);
     const int i = a.i0 + (int)(blockIdx.x / a.ncol);
-    const long sa = (long)(a.off + i) * a.NC + col;
-    const long sb = (long)(a.off + i + a.h) * a.NC + col;
+    long slot[2];
+    slot[0] = (long)(a.off + i) * a.NC + col;
+    slot[1] = (long)(a.off + i + a.h) * a.NC + col;
     const u64 N2 = 2 * a.N;
-    const u64 e = ((u64)i * a.rho) % N2;
-    Rotor<U> rot(c, st, st, 1, l, a.N);
-    i64 xa[2 * U], xb[2 * U];
-    u64 y[U];
-    int tv;
-    load_coeff<U>(c, xa, a.dig, a.top, sa, l);
+    const u64 e = (u32)((u64)i * a.rho) % (u32)N2;
+    i64 x[2][2 * U];
+    u64 ee[2] = {0, 0};
+    bool keep[2] = {true, false};
+    Coef st;
+    st.dig = a.dig;
+    st.cb = a.cb;
+    st.top = a.top;
+    load_coeff<U>(c, x[0], st, slot[0], l);
+    if (a.op != OP_DOUBLE && a.op != OP_FILL) load_coeff<U>(c, x[1], st, slot[1], l);
+    else zero_coeff<U>(x[1]);
     switch (a.op) {
     case OP_DOUBLE:
 #pragma unroll
-        for (int q = 0; q < 2 * U; ++q) xa[q] *= 2;
-        tv = wg_normalize<U>(c, xa, y, l, false, st, scr);
-        store_coeff<U>(c, y, tv, a.dig, a.top, sa, l);
+        for (int q = 0; q < 2 * U; ++q) x[0][q] *= 2;
         break;
     case OP_HALFADD:  // a = (a + b) / 2
-        load_coeff<U>(c, xb, a.dig, a.top, sb, l);
 #pragma unroll
-        for (int q = 0; q < 2 * U; ++q) xa[q] += xb[q];
-        rot(xa, N2 - 1);
-        tv = wg_normalize<U>(c, xa, y, l, false, st, scr);
-        store_coeff<U>(c, y, tv, a.dig, a.top, sa, l);
+        for (int q = 0; q < 2 * U; ++q) x[0][q] += x[1][q];
+        ee[0] = N2 - 1;
+        rotate_set<U, 2>(c, x, ee, a.N, l, sm.stage, 2);
         break;
     case OP_FILL:     // b = 2^e a
-        if (e) rot(xa, e);
-        tv = wg_normalize<U>(c, xa, y, l, false, st, scr);
-        store_coeff<U>(c, y, tv, a.dig, a.top, sb, l);
+#pragma unroll
+        for (int q = 0; q < 2 * U; ++q) x[1][q] = x[0][q];
+        ee[1] = e;
+        rotate_set<U, 2>(c, x, ee, a.N, l, sm.stage, 2);
+        keep[0] = false;
+        keep[1] = true;
         break;
     case OP_FIX:      // d = a - b; b = 2^e d; a = a + d
-        load_coeff<U>(c, xb, a.dig, a.top, sb, l);
 #pragma unroll
         for (int q = 0; q < 2 * U; ++q) {
-            const i64 d = xa[q] - xb[q];
-            xa[q] += d;
-            xb[q] = d;
+            const i64 d = x[0][q] - x[1][q];
+            x[0][q] += d;
+            x[1][q] = d;
         }
-        if (e) rot(xb, e);
-        tv = wg_normalize<U>(c, xa, y, l, false, st, scr);
-        store_coeff<U>(c, y, tv, a.dig, a.top, sa, l);
-        tv = wg_normalize<U>(c, xb, y, l, false, st, scr);
-        store_coeff<U>(c, y, tv, a.dig, a.top, sb, l);
+        ee[1] = e;
+        rotate_set<U, 2>(c, x, ee, a.N, l, sm.stage, 2);
+        keep[1] = true;
         break;
     case OP_TWOXMY:   // a = 2a - b
-        load_coeff<U>(c, xb, a.dig, a.top, sb, l);
 #pragma unroll
-        for (int q = 0; q < 2 * U; ++q) xa[q] = 2 * xa[q] - xb[q];
-        tv = wg_normalize<U>(c, xa, y, l, false, st, scr);
-        store_coeff<U>(c, y, tv, a.dig, a.top, sa, l);
+        for (int q = 0; q < 2 * U; ++q) x[0][q] = 2 * x[0][q] - x[1][q];
         break;
     default:          // OP_IBFLY: t = 2^-e b; a, b = a + t, a - t
-        load_coeff<U>(c, xb, a.dig, a.top, sb, l);
-        if (e) rot(xb, N2 - e);
+        ee[1] = e ? N2 - e : 0;
+        rotate_set<U, 2>(c, x, ee, a.N, l, sm.stage, 2);
 #pragma unroll
         for (int q = 0; q < 2 * U; ++q) {
-            const i64 s = xa[q] + xb[q], d = xa[q] - xb[q];
-            xa[q] = s;
-            xb[q] = d;
+            const i64 s = x[0][q] + x[1][q], d = x[0][q] - x[1][q];
+            x[0][q] = s;
+            x[1][q] = d;
         }
-        tv = wg_normalize<U>(c, xa, y, l, false, st, scr);
-        store_coeff<U>(c, y, tv, a.dig, a.top, sa, l);
-        tv = wg_normalize<U>(c, xb, y, l, false, st, scr);
-        store_coeff<U>(c, y, tv, a.dig, a.top, sb, l);
+        keep[1] = true;
         break;
     }
+    normalize_store<U, 2>(c, x, slot, keep, false, st, l, sm);
 }
 
 // --------------------------------------------------------------------------
 // scaling by 2^-(depth+1) and canonicalisation (mul_fft.c:3256-3260)
 // --------------------------------------------------------------------------
 template <int U>
-__global__ __launch_bounds__(1024) void k_scale(u64 *dig, int *top, int l, u64 N, u64 e)
+__global__ __launch_bounds__(1024) void k_scale(u64 *dig, u64 *cb, int *top, int l, u64 N, u64 e)
 {
+    Coef st;
+    st.dig = dig;
+    st.cb = cb;
+    st.top = top;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const WG c = wg_ctx();
-    i64 *st = (i64 *)smem;
-    u64 *scr = scan_scratch(smem, l, 1);
-    const long slot = blockIdx.x;
-    i64 x[2 * U];
-    u64 y[U];
-    load_coeff<U>(c, x, dig, top, slot, l);
-    Rotor<U> rot(c, st, st, 1, l, N);
-    if (e) rot(x, e);
-    const int tv = wg_normalize<U>(c, x, y, l, true, st, scr);
-    store_coeff<U>(c, y, tv, dig, top, slot, l);
+    const Lds sm = lds_carve<U, 1>(smem, l, 1, c.nw);
+    long slot[1] = {(long)blockIdx.x};
+    bool keep[1] = {true};
+    i64 x[1][2 * U];
+    u64 ee[1] = {e};
+    load_coeff<U>(c, x[0], st, slot[0], l);
+    rotate_set<U, 1>(c, x, ee, N, l, sm.stage, 1);
+    normalize_store<U, 1>(c, x, slot, keep, true, st, l, sm);
 }
 
 // --------------------------------------------------------------------------
@@ -297,16 +336,20 @@ __global__ __launch_bounds__(1024) void k_scale(u64 *dig, int *top, int l, u64 N
 // LDS: A[L] u32, B'[2L] u32 (then reused as normalisation scratch).
 // --------------------------------------------------------------------------
 template <int U>
-__global__ __launch_bounds__(1024) void k_pointwise(u64 *digA, int *topA, const u64 *digB, const int *topB,
-                                                    int l, u64 N)
+__global__ __launch_bounds__(1024) void k_pointwise(u64 *digA, u64 *cbA, int *topA, const u64 *digB,
+                                                    const int *topB, int l, u64 N)
 {
+    Coef st;
+    st.dig = digA;
+    st.cb = cbA;
+    st.top = topA;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const WG c = wg_ctx();
     const int L = 2 * l;
     u32 *As = (u32 *)smem;
     u32 *Bs = As + L;
     u64 *scr = (u64 *)(smem + (size_t)3 * L * sizeof(u32));
-    u64 *ssum = scr + 3 * U * 16 + 4;
+    u64 *ssum = scr + norm_scr_u64(1, U, 16);
     const long slot = blockIdx.x;
     const int ta = topA[slot], tb = topB[slot];  // canonical inputs: tops in {0, 1}
     const u64 *pa = digA + (size_t)slot * l;
@@ -397,9 +440,192 @@ __global__ __launch_bounds__(1024) void k_pointwise(u64 *digA, int *topA, const 
         }
         __syncthreads();
     }
-    u64 y[U];
-    const int tv = wg_normalize<U>(c, d, y, l, true, (i64 *)smem, scr);
-    store_coeff<U>(c, y, tv, digA, topA, slot, l);
+    i64 dd[1][2 * U];
+#pragma unroll
+    for (int q = 0; q < 2 * U; ++q) dd[0][q] = d[q];
+    long slots[1] = {slot};
+    bool keep[1] = {true};
+    Lds sm;
+    sm.stage = nullptr;
+    sm.edge = (int *)smem;                       // As/Bs are dead by now
+    sm.scr = scr;
+    normalize_store<U, 1>(c, dd, slots, keep, true, st, l, sm);
+}
+
+// --------------------------------------------------------------------------
+// k_pw<R>: the register-blocked pointwise product (even l).  Same algebra as
+// k_pointwise; thread t owns the R consecutive columns [R t, R t + R) and walks
+// the L terms 4 at a time: per step one broadcast ds_read_b128 of a[i..i+3], an
+// aligned window of R+4 digits of B' (ds_read_b128, conflict-free across lanes),
+// and 4R multiply-accumulates, each one v_mad_u64_u32 into a 64-bit accumulator
+// whose carry-out feeds a 32-bit high word (v_addc) -- 2 VALU per 32x32 MAC.
+// Columns are then handed to the normaliser's strided limb ownership through LDS.
+// blockDim = L / R (>= 64), U = R / 2 limbs per thread in the normaliser.
+// --------------------------------------------------------------------------
+// four independent 32x32 -> 96-bit multiply-accumulates: acc_k += a * b_k, carry into h_k.
+// Each v_mad_u64_u32 writes its own SGPR-pair carry, read by its v_addc three
+// instructions later (gfx950 needs 2 wait states between a VALU SGPR write and a
+// VALU read of it; the assembler inserts none inside inline asm).
+__device__ __forceinline__ void mac4(u64 &a0, u64 &a1, u64 &a2, u64 &a3, u32 &h0, u32 &h1, u32 &h2, u32 &h3,
+                                     u32 a, u32 b0, u32 b1, u32 b2, u32 b3)
+{
+    u64 c0, c1, c2, c3;
+    asm("v_mad_u64_u32 %0, %8, %12, %13, %0\n\t"
+        "v_mad_u64_u32 %1, %9, %12, %14, %1\n\t"
+        "v_mad_u64_u32 %2, %10, %12, %15, %2\n\t"
+        "v_mad_u64_u32 %3, %11, %12, %16, %3\n\t"
+        "v_addc_co_u32_e64 %4, %8, 0, %4, %8\n\t"
+        "v_addc_co_u32_e64 %5, %9, 0, %5, %9\n\t"
+        "v_addc_co_u32_e64 %6, %10, 0, %6, %10\n\t"
+        "v_addc_co_u32_e64 %7, %11, 0, %7, %11"
+        : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3),
+          "=&s"(c0), "=&s"(c1), "=&s"(c2), "=&s"(c3)
+        : "v"(a), "v"(b0), "v"(b1), "v"(b2), "v"(b3));
+}
+
+template <int R>
+__global__ __launch_bounds__(1024) void k_pw(u64 *digA, u64 *cbA, int *topA, const u64 *digB, const int *topB,
+                                             int l)
+{
+    constexpr int U = R / 2;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const WG c = wg_ctx();
+    const int L = 2 * l;
+    u32 *As = (u32 *)smem;            // L digits of a
+    u32 *Bs = As + L;                 // B'[0, 2L)
+    u64 *scr = (u64 *)(smem + (size_t)3 * L * sizeof(u32));
+    u64 *ssum = scr + norm_scr_u64(1, U, 16);
+    Coef st;
+    st.dig = digA;
+    st.cb = cbA;
+    st.top = topA;
+    const long slot = blockIdx.x;
+    const int ta = topA[slot], tb = topB[slot];  // canonical inputs: tops in {0, 1}
+    const u64 *pa = digA + (size_t)slot * l;
+    const u64 *pb = digB + (size_t)slot * l;
+    if (c.t == 0) *ssum = 0;
+    // strided ownership (normaliser layout): limb m = u * nt + t
+    u64 amine[U];
+    u64 asum = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int m = u * c.nt + c.t;
+        amine[u] = 0;
+        if (m < l) {
+            const u64 va = pa[m], vb = pb[m];
+            amine[u] = va;
+            As[2 * m] = (u32)va;
+            As[2 * m + 1] = (u32)(va >> 32);
+            Bs[L + 2 * m] = (u32)vb;
+            Bs[L + 2 * m + 1] = (u32)(vb >> 32);
+            Bs[2 * m] = ~(u32)vb;
+            Bs[2 * m + 1] = ~(u32)(vb >> 32);
+            asum += (va & MPF_M32) + (va >> 32);
+        }
+    }
+    __syncthreads();
+    i64 d[1][2 * U];
+    if (ta | tb) {
+        // 2^N == -1: the product is -b, -a or 1 (MPIR's c flags, mul_fft.c:3250)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int m = u * c.nt + c.t;
+            d[0][2 * u] = d[0][2 * u + 1] = 0;
+            if (m < l) {
+                if (ta && tb) {
+                    d[0][2 * u] = (m == 0) ? 1 : 0;
+                } else {
+                    const u32 *o = ta ? (Bs + L) : As;
+                    d[0][2 * u] = -(i64)o[2 * m];
+                    d[0][2 * u + 1] = -(i64)o[2 * m + 1];
+                }
+            }
+        }
+        __syncthreads();
+    } else {
+        for (int off = 32; off > 0; off >>= 1) asum += __shfl_xor(asum, off);
+        if (c.lane == 0) atomicAdd((unsigned long long *)ssum, (unsigned long long)asum);
+        const int k0 = R * c.t;
+        u64 acc[R];
+        u32 hh[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            acc[r] = 0;
+            hh[r] = 0;
+        }
+        if (k0 < L) {
+            // window for term block i0: B'[k0 - i0 - 4 + L, +R+4), 16-byte aligned (k0, i0, L = 0 mod 4)
+            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+            const v4u *bw = (const v4u *)(Bs + k0 - 4 + L);
+            const v4u *a4p = (const v4u *)As;
+            constexpr int NW = R / 4 + 1;
+            v4u av = a4p[0];
+            v4u bv[NW];
+#pragma unroll
+            for (int k = 0; k < NW; ++k) {
+                bv[k] = bw[k];
+                asm volatile("" : "+v"(bv[k]));   // keep the whole 16-byte read (one ds_read_b128)
+            }
+            for (int i4 = 0; i4 < L / 4; ++i4) {
+                // prefetch the next block while this one is multiplied
+                const int nx = (i4 + 1 < L / 4) ? i4 + 1 : i4;
+                const v4u avn = a4p[nx];
+                v4u bvn[NW];
+#pragma unroll
+                for (int k = 0; k < NW; ++k) {
+                    bvn[k] = bw[k - nx];
+                    asm volatile("" : "+v"(bvn[k]));
+                }
+                u32 w[4 * NW];
+#pragma unroll
+                for (int k = 0; k < NW; ++k) {
+                    w[4 * k] = bv[k].x; w[4 * k + 1] = bv[k].y; w[4 * k + 2] = bv[k].z; w[4 * k + 3] = bv[k].w;
+                }
+                const u32 a4[4] = {av.x, av.y, av.z, av.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int r = 0; r < R; r += 4)
+                        mac4(acc[r], acc[r + 1], acc[r + 2], acc[r + 3], hh[r], hh[r + 1], hh[r + 2], hh[r + 3],
+                             a4[q], w[4 + r - q], w[5 + r - q], w[6 + r - q], w[7 + r - q]);
+                av = avn;
+#pragma unroll
+                for (int k = 0; k < NW; ++k) bv[k] = bvn[k];
+            }
+        }
+        __syncthreads();  // As/Bs dead: reuse as q0buf[L] u32 + rbuf[L] u64
+        u32 *q0b = (u32 *)smem;
+        u64 *rb = (u64 *)(smem + (size_t)L * sizeof(u32));
+        if (k0 < L) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                q0b[k0 + r] = (u32)acc[r];
+                rb[k0 + r] = (acc[r] >> 32) | ((u64)hh[r] << 32);   // Q_k >> 32  (< 2^45)
+            }
+        }
+        __syncthreads();
+        const i64 S = (i64)*ssum;
+        const i64 rl = (i64)rb[L - 1];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int m = u * c.nt + c.t;
+            d[0][2 * u] = d[0][2 * u + 1] = 0;
+            if (m < l) {
+                const int j = 2 * m;
+                // a b == sum_k (q0_k + r_{k-1}) X^k + S - a, r_{-1} -> -r_{L-1}
+                d[0][2 * u] = (i64)q0b[j] - (i64)(amine[u] & MPF_M32) + (j ? (i64)rb[j - 1] : S - rl);
+                d[0][2 * u + 1] = (i64)q0b[j + 1] - (i64)(amine[u] >> 32) + (i64)rb[j];
+            }
+        }
+        __syncthreads();
+    }
+    long slots[1] = {slot};
+    bool keep[1] = {true};
+    Lds sm;
+    sm.stage = nullptr;
+    sm.edge = (int *)smem;
+    sm.scr = scr;
+    normalize_store<U, 1>(c, d, slots, keep, true, st, l, sm);
 }
 
 // --------------------------------------------------------------------------

@@ -44,7 +44,7 @@ struct Plan {
     long j1, j2, trunc, Tr, len, total;
     int U, tpb, maxlogg;
     size_t slots;       // allocated slots per operand
-    size_t off_digA, off_topA, off_digB, off_topB, off_lo, off_hi, off_bg, off_bp, off_bc, bytes;
+    size_t off_digA, off_topA, off_cbA, off_digB, off_topB, off_cbB, off_lo, off_hi, off_bg, off_bp, off_bc, bytes;
     long nblk;
 };
 
@@ -80,21 +80,24 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
     p->Tr = p->trunc / p->NC;
     p->total = n1 + n2;
     if (p->l > 4096) return MPFFT_EUNSUPPORTED;              // pointwise LDS budget (24 l bytes)
+    // threads per coefficient and limbs per thread: U == 1 kernels are built for
+    // <= 256 threads (MPF_LB), U == 2 / 4 for <= 1024
+    const int Up = p->l <= 256 ? 1 : p->l <= 2048 ? 2 : 4;
     long tpb = 64;
-    while (tpb < p->l && tpb < 1024) tpb *= 2;
-    long U = (p->l + tpb - 1) / tpb;
-    int Up = 1;
-    while (Up < U) Up *= 2;
+    while (tpb * Up < p->l) tpb *= 2;
     p->tpb = (int)tpb;
     p->U = Up;
-    p->maxlogg = Up == 1 ? 4 : Up == 2 ? 3 : Up == 4 ? 2 : 1;
+    p->maxlogg = Up == 1 ? 4 : Up == 2 ? 2 : 1;   // G*U <= 8 keeps U >= 2 passes spill-free
     p->slots = (size_t)2 * p->n;
     size_t o = 0;
     const size_t dig = p->slots * p->l * 8, top = align_up(p->slots * 4, 256);
+    const size_t cbb = align_up(p->slots * cb_words((int)p->l) * 8, 256);
     p->off_digA = o; o += dig;
     p->off_topA = o; o += top;
+    p->off_cbA = o; o += cbb;
     p->off_digB = o; o += dig;
     p->off_topB = o; o += top;
+    p->off_cbB = o; o += cbb;
     p->off_lo = o; o += align_up((size_t)p->total * 8, 256);
     p->off_hi = o; o += align_up((size_t)p->total * 4, 256);
     p->nblk = (p->total + 256 * CARRY_V - 1) / (256 * CARRY_V);
@@ -113,7 +116,7 @@ typedef void (*pass_fn)(PassArgs);
 template <int U>
 static pass_fn pick_pass(int logg, int dir)
 {
-    constexpr int ML = U == 1 ? 4 : U == 2 ? 3 : U == 4 ? 2 : 1;
+    constexpr int ML = U == 1 ? 4 : U == 2 ? 2 : 1;
     if (dir == 0) {
         switch (logg) {
         case 1: return k_pass<U, 1, 0>;
@@ -154,27 +157,37 @@ static thread_local hipError_t last_hip_error = hipSuccess;
 struct Exec {
     const Plan &P;
     hipStream_t s;
-    u64 *digA, *digB;
+    u64 *digA, *digB, *cbA, *cbB;
     int *topA, *topB;
-    int nbuf;
-    size_t lds_pass;
     Exec(const Plan &p, hipStream_t st, unsigned char *ws) : P(p), s(st)
     {
         digA = (u64 *)(ws + P.off_digA);
         topA = (int *)(ws + P.off_topA);
         digB = (u64 *)(ws + P.off_digB);
         topB = (int *)(ws + P.off_topB);
-        const size_t one = (size_t)2 * P.l * sizeof(i64);
-        nbuf = (2 * one <= 64 * 1024) ? 2 : 1;
-        lds_pass = nbuf * one + (3 * P.U * 16 + 8) * sizeof(u64);
+        cbA = (u64 *)(ws + P.off_cbA);
+        cbB = (u64 *)(ws + P.off_cbB);
+        nw = P.tpb / 64;
+    }
+    int nw;
+
+    // rotation staging buffers for a G-coefficient pass: as many as fit in 64 KiB
+    int stage_bufs(int G) const
+    {
+        long fit = (64L * 1024) / (16L * P.l);
+        if (fit < 1) fit = 1;
+        return (int)(fit < G ? fit : G);
     }
 
     int pass(PassArgs a, int logg, int dir, int nops)
     {
         pass_fn f = get_pass(P.U, logg, dir);
         if (!f) return MPFFT_EUNSUPPORTED;
+        const int G = 1 << logg;
+        const int rb = stage_bufs(G);
+        const size_t lds_pass = lds_bytes((int)P.l, rb, G, P.U, nw);
         allow_lds((const void *)f, lds_pass);
-        a.nbuf = nbuf;
+        a.nbuf = rb;
         a.ngroups = 1 << (a.lbM - logg);
         dim3 grid((unsigned)((long)a.nsub * a.ngroups), (unsigned)nops);
         hipLaunchKernelGGL(f, grid, dim3(P.tpb), lds_pass, s, a);
@@ -187,6 +200,7 @@ struct Exec {
         PassArgs a;
         memset(&a, 0, sizeof(a));
         a.dig[0] = digA; a.dig[1] = digB;
+        a.cb[0] = cbA; a.cb[1] = cbB;
         a.top[0] = topA; a.top[1] = topB;
         a.bits1 = P.bits1;
         a.N = P.N;
@@ -248,15 +262,28 @@ struct Exec {
 
     int pointwise()
     {
-        const size_t lds = (size_t)3 * 2 * P.l * 4 + (3 * P.U * 16 + 8) * 8;
-        void (*f)(u64 *, int *, const u64 *, const int *, int, u64) = nullptr;
+        if (P.l % 2 == 0 && P.l >= 32) {   // register-blocked kernel: R columns per thread
+            const int R = P.l >= 2048 ? 8 : 4;
+            const int L = 2 * (int)P.l;
+            const int tpb = (L / R + 63) / 64 * 64;   // whole waves (threads past L/R idle in the MAC loop)
+            const size_t lds = (size_t)3 * L * 4 + (norm_scr_u64(1, R / 2, 16) + 2) * 8;
+            void (*f)(u64 *, u64 *, int *, const u64 *, const int *, int) =
+                R == 8 ? k_pw<8> : k_pw<4>;
+            allow_lds((const void *)f, lds);
+            hipLaunchKernelGGL(f, dim3((unsigned)P.trunc), dim3(tpb), lds, s, digA, cbA, topA, (const u64 *)digB,
+                               (const int *)topB, (int)P.l);
+            HIPCHK(hipGetLastError());
+            return MPFFT_OK;
+        }
+        const size_t lds = (size_t)3 * 2 * P.l * 4 + (norm_scr_u64(1, P.U, 16) + 2) * 8;
+        void (*f)(u64 *, u64 *, int *, const u64 *, const int *, int, u64) = nullptr;
         switch (P.U) {
         case 1: f = k_pointwise<1>; break;
         case 2: f = k_pointwise<2>; break;
         case 4: f = k_pointwise<4>; break;
         }
         allow_lds((const void *)f, lds);
-        hipLaunchKernelGGL(f, dim3((unsigned)P.trunc), dim3(P.tpb), lds, s, digA, topA, (const u64 *)digB,
+        hipLaunchKernelGGL(f, dim3((unsigned)P.trunc), dim3(P.tpb), lds, s, digA, cbA, topA, (const u64 *)digB,
                            (const int *)topB, (int)P.l, P.N);
         HIPCHK(hipGetLastError());
         return MPFFT_OK;
@@ -314,6 +341,7 @@ struct Exec {
         if (cnt <= 0) return MPFFT_OK;
         PairArgs a;
         a.dig = digA;
+        a.cb = cbA;
         a.top = topA;
         a.N = P.N;
         a.l = (int)P.l;
@@ -325,7 +353,7 @@ struct Exec {
         a.i0 = (int)i0;
         a.cnt = (int)cnt;
         a.rho = rho;
-        const size_t lds = (size_t)2 * P.l * sizeof(i64) + (3 * P.U * 16 + 8) * sizeof(u64);
+        const size_t lds = lds_bytes((int)P.l, 2, 2, P.U, nw);
         void (*f)(PairArgs) = nullptr;
         switch (P.U) {
         case 1: f = k_pairop<1>; break;
@@ -377,8 +405,8 @@ struct Exec {
 
     int scale()
     {
-        const size_t lds = (size_t)2 * P.l * sizeof(i64) + (3 * P.U * 16 + 8) * sizeof(u64);
-        void (*f)(u64 *, int *, int, u64, u64) = nullptr;
+        const size_t lds = lds_bytes((int)P.l, 1, 1, P.U, nw);
+        void (*f)(u64 *, u64 *, int *, int, u64, u64) = nullptr;
         switch (P.U) {
         case 1: f = k_scale<1>; break;
         case 2: f = k_scale<2>; break;
@@ -386,7 +414,7 @@ struct Exec {
         }
         const u64 e = 2 * P.N - (u64)(P.depth + 1);
         allow_lds((const void *)f, lds);
-        hipLaunchKernelGGL(f, dim3((unsigned)P.trunc), dim3(P.tpb), lds, s, digA, topA, (int)P.l, P.N, e);
+        hipLaunchKernelGGL(f, dim3((unsigned)P.trunc), dim3(P.tpb), lds, s, digA, cbA, topA, (int)P.l, P.N, e);
         HIPCHK(hipGetLastError());
         return MPFFT_OK;
     }
@@ -456,6 +484,17 @@ size_t mpfft_workspace_bytes(long n1, long n2, unsigned long depth, unsigned lon
     Plan P;
     if (make_plan(&P, n1, n2, depth, w)) return 0;
     return P.bytes;
+}
+
+int mpfft_workspace_layout(long n1, long n2, unsigned long depth, unsigned long w, size_t *out)
+{
+    Plan P;
+    int rc = make_plan(&P, n1, n2, depth, w);
+    if (rc) return rc;
+    out[0] = P.off_digA; out[1] = P.off_topA; out[2] = P.off_cbA;
+    out[3] = P.off_digB; out[4] = P.off_topB; out[5] = P.off_cbB;
+    out[6] = P.slots; out[7] = (size_t)cb_words((int)P.l);
+    return MPFFT_OK;
 }
 
 int mpfft_plan_info(long n1, long n2, unsigned long depth, unsigned long w, long *out)
