@@ -433,7 +433,7 @@ __device__ __forceinline__ i64 rot_digit(const i64 *stage, int j, const Rot &r, 
     const u64 l0 = (u64)(u32)x0 << r.b;
     const u64 l1 = (u64)(u32)x1 << r.b;
     const i64 part0 = (i64)(l0 & MPF_M32);
-    const i64 part1 = (i64)(l1 >> 32) + (x1 >> 32) * ((i64)1 << r.b);
+    const i64 part1 = (i64)(l1 >> 32) + (i64)((u64)(x1 >> 32) << r.b);  // two's complement shift == * 2^b
     return r.sgn * (s0 * part0 + s1 * part1);
 }
 

@@ -72,27 +72,50 @@ __device__ __forceinline__ Lds lds_carve(unsigned char *smem, int l, int rb, int
     return d;
 }
 
-// Multiply x[i] by 2^ee[i] (mod p) for every i with ee[i] != 0.  The rotations are
-// staged rb coefficients at a time through LDS: two barriers per batch.
+// Multiply x[i] by 2^e(i) (mod p) for the i with rot(i) true, e(i) in [0, 2N) uniform.
+// rb >= G: every coefficient owns stage slot i, one write/read round (2 barriers).
+// rb <  G: one coefficient at a time (large coefficients; 2 barriers each).
+template <int U, int G, typename EF>
+__device__ __forceinline__ void rotate_all(const WG &c, i64 (&x)[G][2 * U], EF efn, u64 N, int l, i64 *stage,
+                                           int rb)
+{
+    if (rb >= G) {
+        bool any = false;
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+            const u64 e = efn(i);
+            if (e) {
+                rot_write<U>(c, x[i], stage + (size_t)i * 2 * l, l);
+                any = true;
+            }
+        }
+        if (!any) return;
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+            const u64 e = efn(i);
+            if (e) rot_read<U>(c, x[i], stage + (size_t)i * 2 * l, make_rot(e, N), l);
+        }
+        __syncthreads();
+    } else {
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+            const u64 e = efn(i);
+            if (!e) continue;
+            rot_write<U>(c, x[i], stage, l);
+            __syncthreads();
+            rot_read<U>(c, x[i], stage, make_rot(e, N), l);
+            __syncthreads();
+        }
+    }
+}
+
+// legacy form used by the small kernels (explicit exponent array)
 template <int U, int G>
 __device__ __forceinline__ void rotate_set(const WG &c, i64 (&x)[G][2 * U], const u64 (&ee)[G], u64 N, int l,
                                            i64 *stage, int rb)
 {
-    int slot[G];
-    int cnt = 0;
-#pragma unroll
-    for (int i = 0; i < G; ++i) slot[i] = ee[i] ? cnt++ : -1;
-    for (int b0 = 0; b0 < cnt; b0 += rb) {
-#pragma unroll
-        for (int i = 0; i < G; ++i)
-            if (slot[i] >= b0 && slot[i] < b0 + rb) rot_write<U>(c, x[i], stage + (size_t)(slot[i] - b0) * 2 * l, l);
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < G; ++i)
-            if (slot[i] >= b0 && slot[i] < b0 + rb)
-                rot_read<U>(c, x[i], stage + (size_t)(slot[i] - b0) * 2 * l, make_rot(ee[i], N), l);
-        __syncthreads();
-    }
+    rotate_all<U, G>(c, x, [&](int i) { return ee[i]; }, N, l, stage, rb);
 }
 
 template <int U, int G>
@@ -132,59 +155,57 @@ __global__ __launch_bounds__(MPF_LB(U)) void k_pass(PassArgs a)
     const int bstart = hi << (a.lbM - a.lvl0);
     if (DIR == 0 && bstart >= a.need) return;  // whole block past the truncation point
     const u64 N2 = 2 * a.N;
-    const long sbase = (long)sub * a.sub_stride;
-
-    int pos[G];
-    long slot[G];
-#pragma unroll
-    for (int i = 0; i < G; ++i) {
-        pos[i] = bstart | (i << lobits) | lo;
-        slot[i] = sbase + (long)(a.pos_off + pos[i]) * a.pos_stride;
-    }
+    // position of element i: pos0 + i * pstep; its slot: slot0 + i * sstep
+    const int pos0 = bstart | lo;
+    const int pstep = 1 << lobits;
+    const long slot0 = (long)sub * a.sub_stride + (long)(a.pos_off + pos0) * a.pos_stride;
+    const long sstep = (long)pstep * a.pos_stride;
 
     i64 x[G][2 * U];
 #pragma unroll
     for (int i = 0; i < G; ++i) {
-        if (DIR == 0 && pos[i] >= a.zero_from) zero_coeff<U>(x[i]);
-        else if (a.src[op]) load_split<U>(c, x[i], a.src[op], a.nsrc[op], slot[i], a.bits1, l);
-        else load_coeff<U>(c, x[i], st, slot[i], l);
+        const long sl = slot0 + i * sstep;
+        if (DIR == 0 && pos0 + i * pstep >= a.zero_from) zero_coeff<U>(x[i]);
+        else if (a.src[op]) load_split<U>(c, x[i], a.src[op], a.nsrc[op], sl, a.bits1, l);
+        else load_coeff<U>(c, x[i], st, sl, l);
     }
 
-    const long rsub = (a.tw_mode) ? revbin_dev(sub, a.tw_lbR) : 0;
-    u64 ee[G];
-    if (a.tw_mode == 1) {  // MFA twiddle 2^(w * c * revbin(row)) (README:74-91)
-#pragma unroll
-        for (int i = 0; i < G; ++i) ee[i] = (u32)(a.tw_w * (u64)(a.pos_off + pos[i]) * (u64)rsub) % (u32)N2;
-        rotate_set<U, G>(c, x, ee, a.N, l, sm.stage, a.nbuf);
-    }
+    // MFA twiddles: 2^(tw_w * (pos_off + pos) * revbin(row)), always < 2N
+    const u64 rsub = a.tw_mode ? (u64)revbin_dev(sub, a.tw_lbR) : 0;
+    const u64 tw0 = a.tw_w * (u64)(a.pos_off + pos0) * rsub, twst = a.tw_w * (u64)pstep * rsub;
+    if (a.tw_mode == 1)
+        rotate_all<U, G>(c, x, [&](int i) { return tw0 + (u64)i * twst; }, a.N, l, sm.stage, a.nbuf);
 
 #pragma unroll
     for (int li = 0; li < LOGG; ++li) {
         const int level = DIR == 0 ? a.lvl0 + li : a.lvl0 + LOGG - 1 - li;
-        const int jb = DIR == 0 ? LOGG - 1 - li : li;
+        const int jb = DIR == 0 ? LOGG - 1 - li : li;   // window bit of the butterfly partner
         const int h = 1 << (a.lbM - level - 1);
-        const u32 unit = (u32)(a.rho << level) % (u32)N2;
+        // twiddle of the pair whose upper element is i (bit jb clear):
+        //   (pos_i mod h) * rho 2^level = e0 + (i mod 2^jb) * estep,  always < N
+        const u64 unit = a.rho << level;
+        const u64 e0 = (u64)(pos0 & (h - 1)) * unit;
+        const u64 estep = (u64)pstep * unit;
+        if (DIR == 0) {
 #pragma unroll
-        for (int i = 0; i < G; ++i) ee[i] = 0;
-#pragma unroll
-        for (int i = 0; i < G; ++i) {
-            if ((i >> jb) & 1) continue;
-            const int k = i | (1 << jb);
-            const u64 e = ((u32)(pos[i] & (h - 1)) * unit) % (u32)N2;
-            if (DIR == 0) {
+            for (int i = 0; i < G; ++i) {
+                if ((i >> jb) & 1) continue;
+                const int k = i | (1 << jb);
 #pragma unroll
                 for (int q = 0; q < 2 * U; ++q) {
                     const i64 s = x[i][q] + x[k][q], d = x[i][q] - x[k][q];
                     x[i][q] = s;
                     x[k][q] = d;
                 }
-                ee[k] = e;
-            } else {
-                ee[k] = e ? N2 - e : 0;
             }
-        }
-        rotate_set<U, G>(c, x, ee, a.N, l, sm.stage, a.nbuf);
-        if (DIR == 1) {
+            rotate_all<U, G>(c, x, [&](int k) -> u64 {
+                if (!((k >> jb) & 1)) return 0;
+                return e0 + (u64)(k & ((1 << jb) - 1)) * estep; }, a.N, l, sm.stage, a.nbuf);
+        } else {
+            rotate_all<U, G>(c, x, [&](int k) -> u64 {
+                if (!((k >> jb) & 1)) return 0;
+                const u64 e = e0 + (u64)(k & ((1 << jb) - 1)) * estep;
+                return e ? N2 - e : 0; }, a.N, l, sm.stage, a.nbuf);
 #pragma unroll
             for (int i = 0; i < G; ++i) {
                 if ((i >> jb) & 1) continue;
@@ -199,18 +220,18 @@ __global__ __launch_bounds__(MPF_LB(U)) void k_pass(PassArgs a)
         }
     }
 
-    if (a.tw_mode == 2) {  // inverse MFA twiddle
-#pragma unroll
-        for (int i = 0; i < G; ++i) {
-            const u64 e = (u32)(a.tw_w * (u64)(a.pos_off + pos[i]) * (u64)rsub) % (u32)N2;
-            ee[i] = e ? N2 - e : 0;
-        }
-        rotate_set<U, G>(c, x, ee, a.N, l, sm.stage, a.nbuf);
-    }
+    if (a.tw_mode == 2)
+        rotate_all<U, G>(c, x, [&](int i) -> u64 {
+            const u64 e = tw0 + (u64)i * twst;
+            return e ? N2 - e : 0; }, a.N, l, sm.stage, a.nbuf);
 
+    long slot[G];
     bool keep[G];
 #pragma unroll
-    for (int i = 0; i < G; ++i) keep[i] = DIR == 1 || (pos[i] & ~((1 << lobits) - 1)) < a.need;
+    for (int i = 0; i < G; ++i) {
+        slot[i] = slot0 + i * sstep;
+        keep[i] = DIR == 1 || ((pos0 + i * pstep) & ~(pstep - 1)) < a.need;
+    }
     normalize_store<U, G>(c, x, slot, keep, a.canon != 0, st, l, sm);
 }
 
