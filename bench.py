@@ -42,7 +42,7 @@ CONFIGS = {
 SEED1, SEED2 = 0x1001, 0x2002
 
 STAGE_NAMES = ["fwd_columns", "fwd_rows", "pointwise", "inv_rows", "inv_columns", "scale", "combine"]
-STAGE_KERNEL = {"pointwise": "k_pointwise", "scale": "k_scale"}
+STAGE_KERNEL = {"pointwise": "k_pw<4> (register-blocked asm MAC)", "scale": "k_scale"}
 
 
 def stage_bytes(P, name, n1, n2):

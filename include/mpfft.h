@@ -81,6 +81,41 @@ int mpfft_workspace_layout(long n1, long n2, unsigned long depth, unsigned long 
 int mpfft_stage(int stage, const uint64_t *d_i1, const uint64_t *d_i2, uint64_t *d_r, long n1, long n2,
                 unsigned long depth, unsigned long w, void *d_ws, size_t ws_bytes, void *stream);
 
+/* ---- multi-GPU: one rank's share of a column-sharded multiply (mpir-fft_amd/sharded.py) ----
+ * Column layout (column passes, ITFT, scale): slot = pos * ccount + (c - c0), NR * ccount slots.
+ * Row layout (row passes, pointwise, combine): rows r0 .. r0+rcount of NC/ccb column blocks,
+ *   slot = (c / ccb) * rcount * ccb + (p - r0) * ccb + c % ccb, rcount * NC slots.
+ * Each slot: dig[l] limbs, cb[cb_words] carry masks, top int32. */
+typedef struct mpfft_shard {
+    long n1, n2;
+    unsigned long depth, w;
+    int c0, ccount;           /* columns of the column passes */
+    int r0, rcount;           /* computed row positions of the row passes */
+    int ccb;                  /* columns per block of the row layout (= NC / ranks) */
+    uint64_t *col_dig[2], *col_cb[2];
+    int *col_top[2];
+    uint64_t *row_dig[2], *row_cb[2];
+    int *row_top[2];
+} mpfft_shard;
+
+#define MPFFT_SHARD_FWD_COLUMNS 0   /* split + column DIF of both operands (column layout) */
+#define MPFFT_SHARD_FWD_ROWS 1      /* twiddle + row DIF of both operands (row layout), canonical */
+#define MPFFT_SHARD_POINTWISE 2     /* row layout A <- A * B */
+#define MPFFT_SHARD_INV_ROWS 3      /* row DIT + un-twiddle of A (row layout) */
+#define MPFFT_SHARD_INV_COLUMNS 4   /* truncated column inverse + scale of A (column layout), canonical */
+int mpfft_shard_stage(int stage, const mpfft_shard *sh, const uint64_t *d_i1, const uint64_t *d_i2, void *stream);
+
+/* Combine the canonical coefficients of the row layout (A) into product limbs
+ * [m0, m0+mcount).  kbase = r0 * NC is the first local coefficient; halo holds the
+ * H coefficients before it (contiguous, l limbs each; NULL when kbase == 0).
+ * phase 0: window sums + block flags; d_sum[0..1] = (carry out with carry-in 0,
+ *          every limb propagates) of this rank's range.
+ * phase 1: resolve with carry-in `cin` (from the ranks below) and write d_r[0..mcount). */
+size_t mpfft_shard_combine_tmp_bytes(long mcount);
+int mpfft_shard_combine(const mpfft_shard *sh, int phase, uint64_t *d_r, long m0, long mcount, long kbase,
+                        const uint64_t *halo, int H, void *d_tmp, size_t tmp_bytes, int cin, int *d_sum,
+                        void *stream);
+
 const char *mpfft_strerror(int code);
 int mpfft_version(void);
 

@@ -12,7 +12,8 @@ def load():
     mod = sys.modules.get("mpir_fft_amd")
     if mod is not None:
         return mod
-    spec = importlib.util.spec_from_file_location("mpir_fft_amd", os.path.join(PKG_DIR, "__init__.py"))
+    spec = importlib.util.spec_from_file_location("mpir_fft_amd", os.path.join(PKG_DIR, "__init__.py"),
+                                                  submodule_search_locations=[PKG_DIR])
     mod = importlib.util.module_from_spec(spec)
     sys.modules["mpir_fft_amd"] = mod
     spec.loader.exec_module(mod)

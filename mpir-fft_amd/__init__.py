@@ -30,6 +30,15 @@ _L = ctypes.c_long
 _UL = ctypes.c_ulong
 
 
+class _Shard(ctypes.Structure):
+    """struct mpfft_shard (include/mpfft.h)"""
+    _fields_ = [("n1", ctypes.c_long), ("n2", ctypes.c_long), ("depth", ctypes.c_ulong), ("w", ctypes.c_ulong),
+                ("c0", ctypes.c_int), ("ccount", ctypes.c_int), ("r0", ctypes.c_int), ("rcount", ctypes.c_int),
+                ("ccb", ctypes.c_int),
+                ("col_dig", ctypes.c_void_p * 2), ("col_cb", ctypes.c_void_p * 2), ("col_top", ctypes.c_void_p * 2),
+                ("row_dig", ctypes.c_void_p * 2), ("row_cb", ctypes.c_void_p * 2), ("row_top", ctypes.c_void_p * 2)]
+
+
 class MpfftError(RuntimeError):
     def __init__(self, code, what):
         super().__init__(f"{what}: {strerror(code)} (code {code})")
@@ -74,6 +83,13 @@ def lib():
         h.mpfft_version.restype = ctypes.c_int
         h.mpfft_fill_random.argtypes = [_u64p, _L, ctypes.c_uint64]
         h.mpfft_fill_random.restype = None
+        h.mpfft_shard_stage.argtypes = [ctypes.c_int, ctypes.POINTER(_Shard), _vp, _vp, _vp]
+        h.mpfft_shard_stage.restype = ctypes.c_int
+        h.mpfft_shard_combine_tmp_bytes.argtypes = [_L]
+        h.mpfft_shard_combine_tmp_bytes.restype = ctypes.c_size_t
+        h.mpfft_shard_combine.argtypes = [ctypes.POINTER(_Shard), ctypes.c_int, _vp, _L, _L, _L, _vp, ctypes.c_int,
+                                          _vp, ctypes.c_size_t, ctypes.c_int, _vp, _vp]
+        h.mpfft_shard_combine.restype = ctypes.c_int
         _lib = h
     return _lib
 
@@ -189,3 +205,37 @@ def workspace_views(ws, n1, n2, depth, w):
     def top(off):
         return u8[off:off + slots * 4].view(torch.int32)
     return dig(lay["digA"]), top(lay["topA"]), dig(lay["digB"]), top(lay["topB"])
+
+
+# ---- sharded (multi-GPU) stages: see sharded.py ------------------------------
+
+def shard_desc(sh):
+    """dict from sharded.ShardedMul.shard_desc() -> struct mpfft_shard"""
+    d = _Shard()
+    for k in ("n1", "n2", "depth", "w", "c0", "ccount", "r0", "rcount", "ccb"):
+        setattr(d, k, int(sh[k]))
+    for k in (0, 1):
+        d.col_dig[k] = sh["col"][k]["dig"].data_ptr()
+        d.col_cb[k] = sh["col"][k]["cb"].data_ptr()
+        d.col_top[k] = sh["col"][k]["top"].data_ptr()
+        d.row_dig[k] = sh["row"][k]["dig"].data_ptr()
+        d.row_cb[k] = sh["row"][k]["cb"].data_ptr()
+        d.row_top[k] = sh["row"][k]["top"].data_ptr()
+    return d
+
+
+def shard_stage(which, desc, d_i1, d_i2, stream=None):
+    rc = lib().mpfft_shard_stage(which, ctypes.byref(desc), _ptr(d_i1), _ptr(d_i2), _stream(stream))
+    if rc:
+        raise MpfftError(rc, f"mpfft_shard_stage({which})")
+
+
+def shard_combine_tmp_bytes(mcount):
+    return int(lib().mpfft_shard_combine_tmp_bytes(mcount))
+
+
+def shard_combine(desc, phase, d_r, m0, mcount, kbase, halo, H, tmp, cin, d_sum, stream=None):
+    rc = lib().mpfft_shard_combine(ctypes.byref(desc), phase, _ptr(d_r), m0, mcount, kbase, _ptr(halo), H,
+                                   _ptr(tmp), tmp.numel(), cin, _ptr(d_sum), _stream(stream))
+    if rc:
+        raise MpfftError(rc, f"mpfft_shard_combine(phase {phase})")

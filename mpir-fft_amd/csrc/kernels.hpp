@@ -35,6 +35,10 @@ struct PassArgs {
     u64 rho;             // exponent (bits) of the transform's root at level 0
     long sub_stride, pos_stride;
     int nsub, pos_off;
+    int pbb;             // blocked positions: pos = (blk << pbb) | within, slot += blk * pbs (pbb = 30: none)
+    long pbs;
+    int sub_off;         // global index of sub-array 0 (row for the twiddle, column for the split)
+    long jNC;            // fused split: coefficient index j = (pos_off + pos) * jNC + sub_off + sub
     int zero_from;       // forward: positions >= zero_from are zero inputs
     int need;            // forward: only blocks starting below `need` are live
     int tw_mode;         // 1: pre-multiply by 2^(tw_w*pos*revbin(sub)), 2: post-multiply by its inverse
@@ -155,23 +159,27 @@ __global__ __launch_bounds__(MPF_LB(U)) void k_pass(PassArgs a)
     const int bstart = hi << (a.lbM - a.lvl0);
     if (DIR == 0 && bstart >= a.need) return;  // whole block past the truncation point
     const u64 N2 = 2 * a.N;
-    // position of element i: pos0 + i * pstep; its slot: slot0 + i * sstep
+    // position of element i: pos0 + i * pstep
     const int pos0 = bstart | lo;
     const int pstep = 1 << lobits;
-    const long slot0 = (long)sub * a.sub_stride + (long)(a.pos_off + pos0) * a.pos_stride;
-    const long sstep = (long)pstep * a.pos_stride;
+    const long sbase = (long)sub * a.sub_stride;
+    auto slot_of = [&](int i) -> long {
+        const int ps = a.pos_off + pos0 + i * pstep;
+        return sbase + (long)(ps >> a.pbb) * a.pbs + (long)(ps & ((1 << a.pbb) - 1)) * a.pos_stride;
+    };
 
     i64 x[G][2 * U];
 #pragma unroll
     for (int i = 0; i < G; ++i) {
-        const long sl = slot0 + i * sstep;
         if (DIR == 0 && pos0 + i * pstep >= a.zero_from) zero_coeff<U>(x[i]);
-        else if (a.src[op]) load_split<U>(c, x[i], a.src[op], a.nsrc[op], sl, a.bits1, l);
-        else load_coeff<U>(c, x[i], st, sl, l);
+        else if (a.src[op])
+            load_split<U>(c, x[i], a.src[op], a.nsrc[op],
+                          (long)(a.pos_off + pos0 + i * pstep) * a.jNC + a.sub_off + sub, a.bits1, l);
+        else load_coeff<U>(c, x[i], st, slot_of(i), l);
     }
 
     // MFA twiddles: 2^(tw_w * (pos_off + pos) * revbin(row)), always < 2N
-    const u64 rsub = a.tw_mode ? (u64)revbin_dev(sub, a.tw_lbR) : 0;
+    const u64 rsub = a.tw_mode ? (u64)revbin_dev(a.sub_off + sub, a.tw_lbR) : 0;
     const u64 tw0 = a.tw_w * (u64)(a.pos_off + pos0) * rsub, twst = a.tw_w * (u64)pstep * rsub;
     if (a.tw_mode == 1)
         rotate_all<U, G>(c, x, [&](int i) { return tw0 + (u64)i * twst; }, a.N, l, sm.stage, a.nbuf);
@@ -229,7 +237,7 @@ __global__ __launch_bounds__(MPF_LB(U)) void k_pass(PassArgs a)
     bool keep[G];
 #pragma unroll
     for (int i = 0; i < G; ++i) {
-        slot[i] = slot0 + i * sstep;
+        slot[i] = slot_of(i);
         keep[i] = DIR == 1 || ((pos0 + i * pstep) & ~(pstep - 1)) < a.need;
     }
     normalize_store<U, G>(c, x, slot, keep, a.canon != 0, st, l, sm);
@@ -656,20 +664,52 @@ __global__ __launch_bounds__(1024) void k_pw(u64 *digA, u64 *cbA, int *topA, con
 // The carry chain r = lo + (hi << 64) is then resolved by a device-wide
 // carry-lookahead (k_carry_blocks -> k_carry_scan -> k_carry_apply).
 // --------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_comb_sum(const u64 *dig, int l, u64 N, u64 bits1, long len, long total,
-                                                  u64 *lo64, u32 *hi32)
+struct CombArgs {
+    const u64 *dig;      // canonical coefficients c_k (< 2^N) in the (blocked) row layout
+    int l;
+    u64 N, bits1;
+    long len;            // number of coefficients j1 + j2 - 1
+    long m0, mcount;     // output limbs [m0, m0 + mcount); the kernel also sums limb m0 - 1
+    long kbase;          // first locally stored coefficient (row r0 * NC)
+    const u64 *halo;     // coefficients [kbase - H, kbase) contiguous, or null
+    int H;
+    int NC, cbb, ccb;    // row layout: k -> p = k / NC - r0, c = k % NC,
+    long cbs;            //   slot = (c >> cbb) * cbs + p * ccb + (c & (ccb - 1))
+    long r0;
+    u64 *lo64;           // [mcount + 1]: index i <-> limb m0 - 1 + i
+    u32 *hi32;
+};
+
+__device__ __forceinline__ const u64 *coef_ptr(const CombArgs &a, long k)
 {
-    const long m = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (m >= total) return;
+    if (k < a.kbase) return a.halo + (size_t)(k - (a.kbase - a.H)) * a.l;
+    const long p = k / a.NC - a.r0;
+    const int cc = (int)(k % a.NC);
+    const long slot = (long)(cc >> a.cbb) * a.cbs + p * a.ccb + (cc & (a.ccb - 1));
+    return a.dig + (size_t)slot * a.l;
+}
+
+// per output limb m: the 128-bit sum of the (few) coefficient windows covering
+// bits [64m, 64m + 64)  (FFT_combine_bits, mul_fft.c:207-267)
+__global__ __launch_bounds__(256) void k_comb_sum(CombArgs a)
+{
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > a.mcount) return;
+    const long m = a.m0 - 1 + i;
+    if (m < 0) {
+        a.lo64[i] = 0;
+        a.hi32[i] = 0;
+        return;
+    }
     const u64 P = (u64)m * 64;
-    long klo = (P >= N) ? (long)((P - N) / bits1) : 0;
-    long khi = (long)((P + 63) / bits1);
-    if (khi > len - 1) khi = len - 1;
+    long klo = (P >= a.N) ? (long)((P - a.N) / a.bits1) : 0;
+    long khi = (long)((P + 63) / a.bits1);
+    if (khi > a.len - 1) khi = a.len - 1;
     u64 slo = 0;
     u32 shi = 0;
     for (long k = klo; k <= khi; ++k) {
-        const u64 st = (u64)k * bits1;
-        const u64 *cp = dig + (size_t)k * l;
+        const u64 st = (u64)k * a.bits1;
+        const u64 *cp = coef_ptr(a, k);
         u64 v;
         if (st > P) {
             v = cp[0] << (st - P);
@@ -677,23 +717,23 @@ __global__ __launch_bounds__(256) void k_comb_sum(const u64 *dig, int l, u64 N, 
             const u64 o = P - st;
             const long q = (long)(o >> 6);
             const int s = (int)(o & 63);
-            const u64 w0 = (q < l) ? cp[q] : 0;
-            const u64 w1 = (s && q + 1 < l) ? cp[q + 1] : 0;
+            const u64 w0 = (q < a.l) ? cp[q] : 0;
+            const u64 w1 = (s && q + 1 < a.l) ? cp[q + 1] : 0;
             v = s ? (w0 >> s) | (w1 << (64 - s)) : w0;
         }
         u64 t;
         shi += add_ovf(slo, v, &t);
         slo = t;
     }
-    lo64[m] = slo;
-    hi32[m] = shi;
+    a.lo64[i] = slo;
+    a.hi32[i] = shi;
 }
 
-// limb m of the final sum is e_m = lo64[m] + hi32[m-1]: value v, generate g, propagate p
+// local limb m (0-based) of the final sum is e = lo64[m+1] + hi32[m] (arrays start one limb
+// early): value v, generate g, propagate p
 __device__ __forceinline__ void carry_limb(const u64 *lo64, const u32 *hi32, long m, u64 *v, bool *g, bool *p)
 {
-    const u64 add = m ? hi32[m - 1] : 0;
-    *g = add_ovf(lo64[m], add, v);
+    *g = add_ovf(lo64[m + 1], (u64)hi32[m], v);
     *p = (*v == MPF_MAXL);
 }
 
@@ -738,8 +778,10 @@ __global__ __launch_bounds__(256) void k_carry_blocks(const u64 *lo64, const u32
     }
 }
 
-// single workgroup: carry into every block
-__global__ __launch_bounds__(1024) void k_carry_scan(const u8 *blkG, const u8 *blkP, long nblk, u8 *blkC)
+// single workgroup: carry into every block given the carry `cin` into the first one;
+// sum[0] = carry out of the range with cin = 0, sum[1] = every block propagates
+__global__ __launch_bounds__(1024) void k_carry_scan(const u8 *blkG, const u8 *blkP, long nblk, u8 *blkC,
+                                                     int cin, int *sum)
 {
     __shared__ u64 scr[64];
     const WG c = wg_ctx();
@@ -751,11 +793,25 @@ __global__ __launch_bounds__(1024) void k_carry_scan(const u8 *blkG, const u8 *b
         p = p && blkP[b];
     }
     u32 co;
-    u32 ci = wg_scan<1>(c, g, p, 0, &co, scr);
+    u32 ci = wg_scan<1>(c, g, p, (u32)cin, &co, scr);
     bool run = ci & 1;
     for (long b = b0; b < b0 + per && b < nblk; ++b) {
         blkC[b] = (u8)run;
         run = blkG[b] || (blkP[b] && run);
+    }
+    if (sum) {
+        u32 co0;
+        wg_scan<1>(c, g, p, 0, &co0, scr);
+        const u64 allp = __ballot(p);
+        __shared__ int pall;
+        if (c.t == 0) pall = 1;
+        __syncthreads();
+        if (c.lane == 0 && allp != ~0ull) pall = 0;
+        __syncthreads();
+        if (c.t == 0) {
+            sum[0] = (int)co0;
+            sum[1] = pall;
+        }
     }
 }
 
@@ -778,5 +834,6 @@ __global__ __launch_bounds__(256) void k_carry_apply(const u64 *lo64, const u32 
         carry_limb(lo64, hi32, m, &v, &gk, &pk);
         r[m] = v + (run ? 1 : 0);
         run = gk || (pk && run);
+        (void)pk;
     }
 }

@@ -98,8 +98,8 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
     p->off_digB = o; o += dig;
     p->off_topB = o; o += top;
     p->off_cbB = o; o += cbb;
-    p->off_lo = o; o += align_up((size_t)p->total * 8, 256);
-    p->off_hi = o; o += align_up((size_t)p->total * 4, 256);
+    p->off_lo = o; o += align_up((size_t)(p->total + 1) * 8, 256);
+    p->off_hi = o; o += align_up((size_t)(p->total + 1) * 4, 256);
     p->nblk = (p->total + 256 * CARRY_V - 1) / (256 * CARRY_V);
     p->off_bg = o; o += align_up((size_t)p->nblk, 256);
     p->off_bp = o; o += align_up((size_t)p->nblk, 256);
@@ -154,22 +154,45 @@ static void allow_lds(const void *f, size_t bytes)
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { last_hip_error = e_; return MPFFT_EHIP; } } while (0)
 static thread_local hipError_t last_hip_error = hipSuccess;
 
+// Where one rank's data lives.  The column layout (slot = pos * ccount + c - c0)
+// feeds the column passes; the row layout (rows r0 .. r0 + rcount of `nblk` column
+// blocks of ccb columns: slot = (c / ccb) * rcount * ccb + (p - r0) * ccb + c % ccb)
+// feeds the row passes and the pointwise products.  On one GPU both are the same
+// natural slot-major array (c0 = r0 = 0, ccount = ccb = NC, rcount = T/NC).
+struct View {
+    u64 *dig[2];
+    u64 *cb[2];
+    int *top[2];
+};
+
 struct Exec {
     const Plan &P;
     hipStream_t s;
-    u64 *digA, *digB, *cbA, *cbB;
-    int *topA, *topB;
-    Exec(const Plan &p, hipStream_t st, unsigned char *ws) : P(p), s(st)
-    {
-        digA = (u64 *)(ws + P.off_digA);
-        topA = (int *)(ws + P.off_topA);
-        digB = (u64 *)(ws + P.off_digB);
-        topB = (int *)(ws + P.off_topB);
-        cbA = (u64 *)(ws + P.off_cbA);
-        cbB = (u64 *)(ws + P.off_cbB);
-        nw = P.tpb / 64;
-    }
     int nw;
+    View col, row;
+    int c0, ccount, r0, rcount, ccb, cbb;
+    long cbs;
+
+    Exec(const Plan &p, hipStream_t st) : P(p), s(st) { nw = P.tpb / 64; }
+
+    // single-GPU workspace: both layouts are the natural one
+    void single(unsigned char *ws)
+    {
+        col.dig[0] = (u64 *)(ws + P.off_digA);
+        col.top[0] = (int *)(ws + P.off_topA);
+        col.cb[0] = (u64 *)(ws + P.off_cbA);
+        col.dig[1] = (u64 *)(ws + P.off_digB);
+        col.top[1] = (int *)(ws + P.off_topB);
+        col.cb[1] = (u64 *)(ws + P.off_cbB);
+        row = col;
+        c0 = 0;
+        ccount = (int)P.NC;
+        r0 = 0;
+        rcount = (int)P.Tr;
+        ccb = (int)P.NC;
+        cbb = P.lbC;
+        cbs = (long)P.Tr * P.NC;
+    }
 
     // rotation staging buffers for a G-coefficient pass: as many as fit in 64 KiB
     int stage_bufs(int G) const
@@ -195,16 +218,50 @@ struct Exec {
         return MPFFT_OK;
     }
 
-    PassArgs base_args() const
+    PassArgs base_args(const View &v) const
     {
         PassArgs a;
         memset(&a, 0, sizeof(a));
-        a.dig[0] = digA; a.dig[1] = digB;
-        a.cb[0] = cbA; a.cb[1] = cbB;
-        a.top[0] = topA; a.top[1] = topB;
+        for (int k = 0; k < 2; ++k) {
+            a.dig[k] = v.dig[k];
+            a.cb[k] = v.cb[k];
+            a.top[k] = v.top[k];
+        }
         a.bits1 = P.bits1;
         a.N = P.N;
         a.l = (int)P.l;
+        a.pbb = 30;
+        a.jNC = P.NC;
+        return a;
+    }
+
+    // column layout passes over this rank's ccount columns
+    PassArgs col_args() const
+    {
+        PassArgs a = base_args(col);
+        a.sub_stride = 1;
+        a.pos_stride = ccount;
+        a.nsub = ccount;
+        a.sub_off = c0;
+        return a;
+    }
+
+    // row layout passes over this rank's rcount rows
+    PassArgs row_args() const
+    {
+        PassArgs a = base_args(row);
+        a.lbM = P.lbC;
+        a.rho = (u64)P.w * P.NR;
+        a.sub_stride = ccb;
+        a.pos_stride = 1;
+        a.pbb = cbb;
+        a.pbs = cbs;
+        a.nsub = rcount;
+        a.sub_off = r0;
+        a.zero_from = (int)P.NC;
+        a.need = (int)P.NC;
+        a.tw_w = (u64)P.w;
+        a.tw_lbR = P.lbR;
         return a;
     }
 
@@ -214,7 +271,7 @@ struct Exec {
         int lvl = 0;
         while (lvl < P.lbR) {
             int k = P.lbR - lvl < P.maxlogg ? P.lbR - lvl : P.maxlogg;
-            PassArgs a = base_args();
+            PassArgs a = col_args();
             if (lvl == 0) {
                 a.src[0] = srcA; a.nsrc[0] = nA;
                 a.src[1] = srcB; a.nsrc[1] = nB;
@@ -225,9 +282,6 @@ struct Exec {
             a.lbM = P.lbR;
             a.lvl0 = lvl;
             a.rho = (u64)P.w * P.NC;
-            a.sub_stride = 1;
-            a.pos_stride = P.NC;
-            a.nsub = (int)P.NC;
             a.need = (int)P.Tr;
             int rc = pass(a, k, 0, nops);
             if (rc) return rc;
@@ -242,16 +296,9 @@ struct Exec {
         int lvl = 0;
         while (lvl < P.lbC) {
             int k = P.lbC - lvl < P.maxlogg ? P.lbC - lvl : P.maxlogg;
-            PassArgs a = base_args();
-            a.lbM = P.lbC;
+            PassArgs a = row_args();
             a.lvl0 = lvl;
-            a.rho = (u64)P.w * P.NR;
-            a.sub_stride = P.NC;
-            a.pos_stride = 1;
-            a.nsub = (int)P.Tr;
-            a.zero_from = (int)P.NC;
-            a.need = (int)P.NC;
-            if (lvl == 0) { a.tw_mode = 1; a.tw_w = (u64)P.w; a.tw_lbR = P.lbR; }
+            a.tw_mode = lvl == 0 ? 1 : 0;
             if (lvl + k == P.lbC) a.canon = 1;
             int rc = pass(a, k, 0, nops);
             if (rc) return rc;
@@ -262,16 +309,17 @@ struct Exec {
 
     int pointwise()
     {
+        const long cnt = (long)rcount * P.NC;
+        if (cnt == 0) return MPFFT_OK;
         if (P.l % 2 == 0 && P.l >= 32) {   // register-blocked kernel: R columns per thread
             const int R = P.l >= 2048 ? 8 : 4;
             const int L = 2 * (int)P.l;
             const int tpb = (L / R + 63) / 64 * 64;   // whole waves (threads past L/R idle in the MAC loop)
             const size_t lds = (size_t)3 * L * 4 + (norm_scr_u64(1, R / 2, 16) + 2) * 8;
-            void (*f)(u64 *, u64 *, int *, const u64 *, const int *, int) =
-                R == 8 ? k_pw<8> : k_pw<4>;
+            void (*f)(u64 *, u64 *, int *, const u64 *, const int *, int) = R == 8 ? k_pw<8> : k_pw<4>;
             allow_lds((const void *)f, lds);
-            hipLaunchKernelGGL(f, dim3((unsigned)P.trunc), dim3(tpb), lds, s, digA, cbA, topA, (const u64 *)digB,
-                               (const int *)topB, (int)P.l);
+            hipLaunchKernelGGL(f, dim3((unsigned)cnt), dim3(tpb), lds, s, row.dig[0], row.cb[0], row.top[0],
+                               (const u64 *)row.dig[1], (const int *)row.top[1], (int)P.l);
             HIPCHK(hipGetLastError());
             return MPFFT_OK;
         }
@@ -283,8 +331,8 @@ struct Exec {
         case 4: f = k_pointwise<4>; break;
         }
         allow_lds((const void *)f, lds);
-        hipLaunchKernelGGL(f, dim3((unsigned)P.trunc), dim3(P.tpb), lds, s, digA, cbA, topA, (const u64 *)digB,
-                           (const int *)topB, (int)P.l, P.N);
+        hipLaunchKernelGGL(f, dim3((unsigned)cnt), dim3(P.tpb), lds, s, row.dig[0], row.cb[0], row.top[0],
+                           (const u64 *)row.dig[1], (const int *)row.top[1], (int)P.l, P.N);
         HIPCHK(hipGetLastError());
         return MPFFT_OK;
     }
@@ -295,16 +343,9 @@ struct Exec {
         int hi = P.lbC;
         while (hi > 0) {
             int k = hi < P.maxlogg ? hi : P.maxlogg;
-            PassArgs a = base_args();
-            a.lbM = P.lbC;
+            PassArgs a = row_args();
             a.lvl0 = hi - k;
-            a.rho = (u64)P.w * P.NR;
-            a.sub_stride = P.NC;
-            a.pos_stride = 1;
-            a.nsub = (int)P.Tr;
-            a.zero_from = (int)P.NC;
-            a.need = (int)P.NC;
-            if (hi - k == 0) { a.tw_mode = 2; a.tw_w = (u64)P.w; a.tw_lbR = P.lbR; }
+            a.tw_mode = (hi - k == 0) ? 2 : 0;
             int rc = pass(a, k, 1, 1);
             if (rc) return rc;
             hi -= k;
@@ -312,20 +353,17 @@ struct Exec {
         return MPFFT_OK;
     }
 
-    // full inverse (DIT) over block [off, off + m) of every column
+    // full inverse (DIT) over block [off, off + m) of every local column
     int ifft_block(long off, long m)
     {
         const int lbM = ilog2(m);
         int hi = lbM;
         while (hi > 0) {
             int k = hi < P.maxlogg ? hi : P.maxlogg;
-            PassArgs a = base_args();
+            PassArgs a = col_args();
             a.lbM = lbM;
             a.lvl0 = hi - k;
-            a.rho = (u64)P.w * P.NC * (u64)(P.NR / m);
-            a.sub_stride = 1;
-            a.pos_stride = P.NC;
-            a.nsub = (int)P.NC;
+            a.rho = rho_blk(m);
             a.pos_off = (int)off;
             a.zero_from = (int)m;
             a.need = (int)m;
@@ -340,14 +378,14 @@ struct Exec {
     {
         if (cnt <= 0) return MPFFT_OK;
         PairArgs a;
-        a.dig = digA;
-        a.cb = cbA;
-        a.top = topA;
+        a.dig = col.dig[0];
+        a.cb = col.cb[0];
+        a.top = col.top[0];
         a.N = P.N;
         a.l = (int)P.l;
         a.op = op;
-        a.NC = P.NC;
-        a.ncol = (int)P.NC;
+        a.NC = ccount;
+        a.ncol = ccount;
         a.off = (int)off;
         a.h = (int)h;
         a.i0 = (int)i0;
@@ -361,7 +399,7 @@ struct Exec {
         case 4: f = k_pairop<4>; break;
         }
         allow_lds((const void *)f, lds);
-        hipLaunchKernelGGL(f, dim3((unsigned)(cnt * P.NC)), dim3(P.tpb), lds, s, a);
+        hipLaunchKernelGGL(f, dim3((unsigned)(cnt * ccount)), dim3(P.tpb), lds, s, a);
         HIPCHK(hipGetLastError());
         return MPFFT_OK;
     }
@@ -405,6 +443,7 @@ struct Exec {
 
     int scale()
     {
+        const long cnt = (long)P.Tr * ccount;
         const size_t lds = lds_bytes((int)P.l, 1, 1, P.U, nw);
         void (*f)(u64 *, u64 *, int *, int, u64, u64) = nullptr;
         switch (P.U) {
@@ -414,34 +453,70 @@ struct Exec {
         }
         const u64 e = 2 * P.N - (u64)(P.depth + 1);
         allow_lds((const void *)f, lds);
-        hipLaunchKernelGGL(f, dim3((unsigned)P.trunc), dim3(P.tpb), lds, s, digA, cbA, topA, (int)P.l, P.N, e);
+        hipLaunchKernelGGL(f, dim3((unsigned)cnt), dim3(P.tpb), lds, s, col.dig[0], col.cb[0], col.top[0],
+                           (int)P.l, P.N, e);
         HIPCHK(hipGetLastError());
         return MPFFT_OK;
     }
 
-    int combine(u64 *r, unsigned char *ws)
+    // combine the canonical coefficients of the row layout (A) into limbs [m0, m0+mcount)
+    // with carry-in `cin`; tmp arrays: lo (mcount+1 u64), hi (mcount+1 u32), 3 block-flag
+    // arrays of nblk bytes, sum[2] int.
+    int combine(u64 *r, long m0, long mcount, long kbase, const u64 *halo, int H, u64 *lo, u32 *hi, u8 *bg,
+                u8 *bp, u8 *bc, int cin, int *sum, bool apply)
     {
-        u64 *lo = (u64 *)(ws + P.off_lo);
-        u32 *hi = (u32 *)(ws + P.off_hi);
-        u8 *bg = ws + P.off_bg, *bp = ws + P.off_bp, *bc = ws + P.off_bc;
-        hipLaunchKernelGGL(k_comb_sum, dim3((unsigned)((P.total + 255) / 256)), dim3(256), 0, s,
-                           (const u64 *)digA, (int)P.l, P.N, P.bits1, P.len, P.total, lo, hi);
+        const long nblk = (mcount + 256 * CARRY_V - 1) / (256 * CARRY_V);
+        if (!apply) {
+            CombArgs a;
+            a.dig = row.dig[0];
+            a.l = (int)P.l;
+            a.N = P.N;
+            a.bits1 = P.bits1;
+            a.len = P.len;
+            a.m0 = m0;
+            a.mcount = mcount;
+            a.kbase = kbase;
+            a.halo = halo;
+            a.H = H;
+            a.NC = (int)P.NC;
+            a.cbb = cbb;
+            a.ccb = ccb;
+            a.cbs = cbs;
+            a.r0 = r0;
+            a.lo64 = lo;
+            a.hi32 = hi;
+            hipLaunchKernelGGL(k_comb_sum, dim3((unsigned)((mcount + 1 + 255) / 256)), dim3(256), 0, s, a);
+            HIPCHK(hipGetLastError());
+            hipLaunchKernelGGL(k_carry_blocks, dim3((unsigned)nblk), dim3(256), 0, s, (const u64 *)lo,
+                               (const u32 *)hi, mcount, bg, bp);
+            HIPCHK(hipGetLastError());
+            if (sum) {   // rank summary only (carry-in decided by the caller)
+                hipLaunchKernelGGL(k_carry_scan, dim3(1), dim3(1024), 0, s, (const u8 *)bg, (const u8 *)bp, nblk,
+                                   bc, 0, sum);
+                HIPCHK(hipGetLastError());
+                return MPFFT_OK;
+            }
+        }
+        hipLaunchKernelGGL(k_carry_scan, dim3(1), dim3(1024), 0, s, (const u8 *)bg, (const u8 *)bp, nblk, bc, cin,
+                           (int *)nullptr);
         HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_carry_blocks, dim3((unsigned)P.nblk), dim3(256), 0, s, (const u64 *)lo,
-                           (const u32 *)hi, P.total, bg, bp);
-        HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_carry_scan, dim3(1), dim3(1024), 0, s, (const u8 *)bg, (const u8 *)bp, P.nblk, bc);
-        HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_carry_apply, dim3((unsigned)P.nblk), dim3(256), 0, s, (const u64 *)lo,
-                           (const u32 *)hi, P.total, (const u8 *)bc, r);
+        hipLaunchKernelGGL(k_carry_apply, dim3((unsigned)nblk), dim3(256), 0, s, (const u64 *)lo, (const u32 *)hi,
+                           mcount, (const u8 *)bc, r);
         HIPCHK(hipGetLastError());
         return MPFFT_OK;
+    }
+
+    int combine_single(u64 *r, unsigned char *ws)
+    {
+        return combine(r, 0, P.total, 0, nullptr, 0, (u64 *)(ws + P.off_lo), (u32 *)(ws + P.off_hi),
+                       ws + P.off_bg, ws + P.off_bp, ws + P.off_bc, 0, nullptr, false);
     }
 };
 
 static int run_all(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, unsigned char *ws, hipStream_t s)
 {
-    Exec X(P, s, ws);
+    Exec X(P, s);
+    X.single(ws);
     int rc;
     if ((rc = X.fwd_columns(d_i1, P.n1, d_i2, P.n2, 2))) return rc;
     if ((rc = X.fwd_rows(2))) return rc;
@@ -449,7 +524,7 @@ static int run_all(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, un
     if ((rc = X.inv_rows())) return rc;
     if ((rc = X.itft(0, P.NR, P.Tr))) return rc;
     if ((rc = X.scale())) return rc;
-    return X.combine(d_r, ws);
+    return X.combine_single(d_r, ws);
 }
 
 // ---------------------------------------------------------------------------
@@ -528,7 +603,8 @@ int mpfft_stage(int stage, const uint64_t *d_i1, const uint64_t *d_i2, uint64_t 
     if (rc) return rc;
     if (!d_ws || ws_bytes < P.bytes) return MPFFT_ENOMEM;
     (void)hipGetLastError();
-    Exec X(P, (hipStream_t)stream, (unsigned char *)d_ws);
+    Exec X(P, (hipStream_t)stream);
+    X.single((unsigned char *)d_ws);
     switch (stage) {
     case MPFFT_STAGE_FWD_COLUMNS: return X.fwd_columns(d_i1, n1, d_i2, n2, 2);
     case MPFFT_STAGE_FWD_ROWS: return X.fwd_rows(2);
@@ -536,9 +612,83 @@ int mpfft_stage(int stage, const uint64_t *d_i1, const uint64_t *d_i2, uint64_t 
     case MPFFT_STAGE_INV_ROWS: return X.inv_rows();
     case MPFFT_STAGE_INV_COLUMNS: return X.itft(0, P.NR, P.Tr);
     case MPFFT_STAGE_SCALE: return X.scale();
-    case MPFFT_STAGE_COMBINE: return X.combine(d_r, (unsigned char *)d_ws);
+    case MPFFT_STAGE_COMBINE: return X.combine_single(d_r, (unsigned char *)d_ws);
     }
     return MPFFT_EINVAL;
+}
+
+// ---- sharded multi-GPU stages ------------------------------------------------
+static int shard_exec(Exec &X, const mpfft_shard *sh)
+{
+    const Plan &P = X.P;
+    if (sh->ccount < 1 || sh->c0 < 0 || sh->c0 + sh->ccount > P.NC) return MPFFT_EINVAL;
+    if (sh->rcount < 0 || sh->r0 < 0 || sh->r0 + sh->rcount > P.Tr) return MPFFT_EINVAL;
+    if (sh->ccb < 1 || P.NC % sh->ccb || (sh->ccb & (sh->ccb - 1))) return MPFFT_EINVAL;
+    for (int k = 0; k < 2; ++k) {
+        X.col.dig[k] = sh->col_dig[k];
+        X.col.cb[k] = sh->col_cb[k];
+        X.col.top[k] = sh->col_top[k];
+        X.row.dig[k] = sh->row_dig[k];
+        X.row.cb[k] = sh->row_cb[k];
+        X.row.top[k] = sh->row_top[k];
+    }
+    X.c0 = sh->c0;
+    X.ccount = sh->ccount;
+    X.r0 = sh->r0;
+    X.rcount = sh->rcount;
+    X.ccb = sh->ccb;
+    X.cbb = ilog2(sh->ccb);
+    X.cbs = (long)sh->rcount * sh->ccb;
+    return MPFFT_OK;
+}
+
+int mpfft_shard_stage(int stage, const mpfft_shard *sh, const uint64_t *d_i1, const uint64_t *d_i2, void *stream)
+{
+    Plan P;
+    int rc = make_plan(&P, sh->n1, sh->n2, sh->depth, sh->w);
+    if (rc) return rc;
+    (void)hipGetLastError();
+    Exec X(P, (hipStream_t)stream);
+    if ((rc = shard_exec(X, sh))) return rc;
+    switch (stage) {
+    case MPFFT_SHARD_FWD_COLUMNS: return X.fwd_columns(d_i1, sh->n1, d_i2, sh->n2, 2);
+    case MPFFT_SHARD_FWD_ROWS: return X.rcount ? X.fwd_rows(2) : MPFFT_OK;
+    case MPFFT_SHARD_POINTWISE: return X.pointwise();
+    case MPFFT_SHARD_INV_ROWS: return X.rcount ? X.inv_rows() : MPFFT_OK;
+    case MPFFT_SHARD_INV_COLUMNS:
+        if ((rc = X.itft(0, P.NR, P.Tr))) return rc;
+        return X.scale();
+    }
+    return MPFFT_EINVAL;
+}
+
+size_t mpfft_shard_combine_tmp_bytes(long mcount)
+{
+    const long nblk = (mcount + 256 * CARRY_V - 1) / (256 * CARRY_V);
+    return align_up((size_t)(mcount + 1) * 8, 256) + align_up((size_t)(mcount + 1) * 4, 256) +
+           3 * align_up((size_t)nblk, 256);
+}
+
+int mpfft_shard_combine(const mpfft_shard *sh, int phase, uint64_t *d_r, long m0, long mcount, long kbase,
+                        const uint64_t *halo, int H, void *d_tmp, size_t tmp_bytes, int cin, int *d_sum,
+                        void *stream)
+{
+    Plan P;
+    int rc = make_plan(&P, sh->n1, sh->n2, sh->depth, sh->w);
+    if (rc) return rc;
+    if (mcount < 1 || m0 < 0 || m0 + mcount > P.total) return MPFFT_EINVAL;
+    if (tmp_bytes < mpfft_shard_combine_tmp_bytes(mcount)) return MPFFT_ENOMEM;
+    (void)hipGetLastError();
+    Exec X(P, (hipStream_t)stream);
+    if ((rc = shard_exec(X, sh))) return rc;
+    unsigned char *t = (unsigned char *)d_tmp;
+    const long nblk = (mcount + 256 * CARRY_V - 1) / (256 * CARRY_V);
+    u64 *lo = (u64 *)t;
+    u32 *hi = (u32 *)(t + align_up((size_t)(mcount + 1) * 8, 256));
+    u8 *bg = (u8 *)hi + align_up((size_t)(mcount + 1) * 4, 256);
+    u8 *bp = bg + align_up((size_t)nblk, 256);
+    u8 *bc = bp + align_up((size_t)nblk, 256);
+    return X.combine(d_r, m0, mcount, kbase, halo, H, lo, hi, bg, bp, bc, cin, d_sum, phase == 1);
 }
 
 // host-pointer entry with status

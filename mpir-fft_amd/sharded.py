@@ -1,0 +1,265 @@
+"""Column-sharded new_mpn_mul over the ranks of a torch.distributed group
+(BASELINE configs[4]: "MFA columns sharded 8-way with RCCL all-to-all over xGMI
+between the column and row passes").
+
+The matrix Fourier algorithm's column transforms are independent per column
+(/root/reference/mul_fft.c:2374-2390) and its row transforms, pointwise products
+and row inverses are independent per row (:2392-2408, :3244-3253, :2942-2957).
+So:
+
+  rank g owns columns [g*C, (g+1)*C), C = NC / world     (column layout)
+  1. split + forward column passes of both operands on the owned columns
+  2. all-to-all #1: rows [r_d, r_{d+1}) of every column block -> rank d
+  3. twiddle + forward row passes, pointwise, inverse row passes on owned rows
+  4. all-to-all #2: the rows go back to their column owners
+  5. truncated inverse column transform + scaling on the owned columns
+  6. all-to-all #3: contiguous coefficient ranges -> rank d; all-gather of a
+     small halo (the few coefficients overlapping the rank's first limbs)
+  7. combine the rank's limb range; all-gather of one (generate, propagate)
+     pair per rank resolves the cross-rank carry (a scan over ranks)
+
+The product ends up distributed: rank d holds limbs [M_d, M_{d+1}).  Exchanges
+use all_to_all_single (RCCL over xGMI on GPUs, gloo on CPU for the tests);
+no all-reduce is used.  Each exchange moves one copy of the data: #1 both
+operands, #2 and #3 one.
+"""
+import math
+
+import numpy as np
+
+
+def cb_words(l):
+    return 2 * ((l + 63) // 64)
+
+
+class ShardPlan:
+    """Partition of one multiply over `world` ranks (pure host arithmetic)."""
+
+    def __init__(self, mp, n1, n2, depth, w, world):
+        P = mp.plan_info(n1, n2, depth, w)
+        self.n1, self.n2, self.depth, self.w, self.world = n1, n2, depth, w, world
+        self.n, self.l, self.NC, self.NR = P["n"], P["l"], P["NC"], P["NR"]
+        self.T, self.bits1 = P["trunc"], P["bits1"]
+        self.N = self.n * w
+        self.len = P["j1"] + P["j2"] - 1
+        self.Tr = self.T // self.NC
+        if self.NC % world or world & (world - 1):
+            raise ValueError(f"world={world} must be a power of two dividing NC={self.NC}")
+        self.C = self.NC // world                     # columns per rank (= column block of the row layout)
+        self.rows = [(d * self.Tr) // world for d in range(world + 1)]
+        self.total = n1 + n2
+        # output limb ranges: rank d starts at the first limb of coefficient r_d * NC
+        self.M = [0] + [min(self.total, (self.rows[d] * self.NC * self.bits1) // 64) for d in range(1, world)] \
+            + [self.total]
+        # coefficients overlapping limbs >= M_d - 1 that precede rank d's first coefficient
+        self.H = math.ceil((self.N + 128) / self.bits1) + 1
+        self.cbw = cb_words(self.l)
+        for d in range(1, world):
+            if self.rows[d] * self.NC < self.H:
+                raise ValueError("too many ranks for this size (halo spans ranks)")
+            if self.rows[d + 1] - self.rows[d] < 1:
+                raise ValueError("a rank owns no rows")
+
+    def rcount(self, d):
+        return self.rows[d + 1] - self.rows[d]
+
+    def col_slots(self):
+        return self.NR * self.C
+
+    def row_slots(self, d):
+        return self.rcount(d) * self.NC
+
+
+class ShardedMul:
+    """One rank's part.  `backend` runs the stages on this rank's buffers,
+    `comm` moves them (both duck-typed; see GpuBackend / TorchComm)."""
+
+    def __init__(self, plan, rank, backend, comm):
+        self.p, self.rank, self.be, self.comm = plan, rank, backend, comm
+        p = plan
+        self.col = [backend.alloc_coeffs(p.col_slots()) for _ in range(2)]
+        self.row = [backend.alloc_coeffs(p.row_slots(rank)) for _ in range(2)]
+
+    def shard_desc(self):
+        p, d = self.p, self.rank
+        return dict(n1=p.n1, n2=p.n2, depth=p.depth, w=p.w, c0=d * p.C, ccount=p.C,
+                    r0=p.rows[d], rcount=p.rcount(d), ccb=p.C, col=self.col, row=self.row)
+
+    # all-to-all #1 / #3: column layout rows [r_d, r_{d+1}) -> rank d's row layout block
+    def _col_to_row(self, k, fields):
+        p = self.p
+        ins = [p.rcount(d) * p.C for d in range(p.world)]            # slots sent to each rank
+        outs = [p.rcount(self.rank) * p.C] * p.world                  # slots received from each rank
+        n_in = sum(ins)
+        for f in fields:
+            self.comm.all_to_all(self.row[k][f], self.col[k][f][: n_in * self.be.width(f, p)],
+                                 [s * self.be.width(f, p) for s in outs], [s * self.be.width(f, p) for s in ins])
+
+    # all-to-all #2: row layout block s -> rank s's column layout rows [r_d, r_{d+1})
+    def _row_to_col(self, k, fields):
+        p = self.p
+        ins = [p.rcount(self.rank) * p.C] * p.world
+        outs = [p.rcount(d) * p.C for d in range(p.world)]
+        n_out = sum(outs)
+        for f in fields:
+            self.comm.all_to_all(self.col[k][f][: n_out * self.be.width(f, p)], self.row[k][f],
+                                 [s * self.be.width(f, p) for s in outs], [s * self.be.width(f, p) for s in ins])
+
+    def run(self, i1, i2):
+        """i1, i2: full operands on this rank (backend arrays).  Returns (m0, limbs)."""
+        p, be, sh = self.p, self.be, self.shard_desc()
+        be.stage("fwd_columns", sh, i1, i2)
+        for k in (0, 1):
+            self._col_to_row(k, ("dig", "cb", "top"))
+        be.stage("fwd_rows", sh, i1, i2)
+        be.stage("pointwise", sh, i1, i2)
+        be.stage("inv_rows", sh, i1, i2)
+        self._row_to_col(0, ("dig", "cb", "top"))
+        be.stage("inv_columns", sh, i1, i2)
+        self._col_to_row(0, ("dig",))                      # canonical coefficients: limbs only
+        # halo: the last H coefficients of every rank's range, all-gathered
+        halo_all = self.comm.all_gather(be.tail_coeffs(sh, p.H))
+        d = self.rank
+        m0, mcount = p.M[d], p.M[d + 1] - p.M[d]
+        kbase = p.rows[d] * p.NC
+        halo = halo_all[d - 1] if d > 0 else None
+        summary = be.combine(sh, 0, m0, mcount, kbase, halo, p.H if d else 0, cin=0)
+        sums = self.comm.all_gather(summary)               # (generate, propagate) per rank
+        cin = 0
+        for e in range(d):
+            g, pr = int(sums[e][0]), int(sums[e][1])
+            cin = 1 if (g or (pr and cin)) else 0
+        limbs = be.combine(sh, 1, m0, mcount, kbase, halo, p.H if d else 0, cin=cin)
+        return m0, limbs
+
+
+class TorchComm:
+    """torch.distributed exchanges.  host_staging=True routes GPU tensors through the
+    host (gloo on one GPU box / CPU tests); otherwise RCCL moves device buffers over xGMI."""
+
+    def __init__(self, host_staging=False):
+        import torch.distributed as dist
+        self.dist = dist
+        self.host = host_staging
+
+    def all_to_all(self, out, inp, out_splits, in_splits):
+        if self.host and out.is_cuda:
+            o = out.cpu()
+            self.dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits)
+            out.copy_(o)
+        else:
+            self.dist.all_to_all_single(out, inp, out_splits, in_splits)
+
+    def all_gather(self, t):
+        import torch
+        src = t.cpu() if (self.host and t.is_cuda) else t
+        bufs = [torch.empty_like(src) for _ in range(self.dist.get_world_size())]
+        self.dist.all_gather(bufs, src.contiguous())
+        return bufs
+
+
+class GpuBackend:
+    """Stages through libmpfft's mpfft_shard_* C ABI on torch device buffers."""
+
+    def __init__(self, mp, plan, device, stream=None):
+        import torch
+        self.mp, self.p, self.dev, self.torch = mp, plan, device, torch
+        self.stream = stream
+        self._tmp = None
+
+    def width(self, field, p):
+        return {"dig": p.l, "cb": p.cbw, "top": 1}[field]
+
+    def alloc_coeffs(self, slots):
+        t = self.torch
+        p = self.p
+        return {"dig": t.empty(slots * p.l, dtype=t.int64, device=self.dev),
+                "cb": t.zeros(slots * p.cbw, dtype=t.int64, device=self.dev),
+                "top": t.zeros(slots, dtype=t.int32, device=self.dev)}
+
+    def _desc(self, sh):
+        return self.mp.shard_desc(sh)
+
+    def stage(self, name, sh, i1, i2):
+        which = {"fwd_columns": 0, "fwd_rows": 1, "pointwise": 2, "inv_rows": 3, "inv_columns": 4}[name]
+        self.mp.shard_stage(which, self._desc(sh), i1, i2, self.stream)
+
+    def tail_coeffs(self, sh, H):
+        """canonical limbs of the last H coefficients of this rank's range (row layout)."""
+        p = self.p
+        r0, rc, C = sh["r0"], sh["rcount"], sh["ccb"]
+        ks = np.arange((r0 + rc) * p.NC - H, (r0 + rc) * p.NC)
+        pp, cc = ks // p.NC - r0, ks % p.NC
+        slots = (cc // C) * (rc * C) + pp * C + (cc % C)
+        dig = sh["row"][0]["dig"].view(-1, p.l)
+        idx = self.torch.as_tensor(slots, device=self.dev, dtype=self.torch.int64)
+        return dig.index_select(0, idx).reshape(-1).contiguous()
+
+    def combine(self, sh, phase, m0, mcount, kbase, halo, H, cin):
+        t = self.torch
+        nb = self.mp.shard_combine_tmp_bytes(mcount)
+        if self._tmp is None or self._tmp.numel() < nb:
+            self._tmp = t.empty(nb, dtype=t.uint8, device=self.dev)
+        if phase == 0:
+            self._sum = t.zeros(2, dtype=t.int32, device=self.dev)
+            self._r = t.empty(mcount, dtype=t.int64, device=self.dev)
+            halo_d = halo.to(self.dev) if halo is not None else None
+            self._halo = halo_d
+            self.mp.shard_combine(self._desc(sh), 0, self._r, m0, mcount, kbase, halo_d, H, self._tmp, cin,
+                                  self._sum, self.stream)
+            return self._sum
+        self.mp.shard_combine(self._desc(sh), 1, self._r, m0, mcount, kbase, self._halo, H, self._tmp, cin,
+                              self._sum, self.stream)
+        return self._r
+
+
+def bench(args, cfg, rank, world, dev):
+    """`bench.py --mode sharded`: one multiply of config `cfg` split over all ranks."""
+    import json  # noqa: F401
+    import time
+
+    import torch
+    import torch.distributed as dist
+    import mpfft_loader
+    mp = mpfft_loader.load()
+    depth, w, nl = cfg
+    plan = ShardPlan(mp, nl, nl, depth, w, world)
+    a = mp.fill_random(nl, 0x1001)
+    b = mp.fill_random(nl, 0x2002)
+    da = torch.from_numpy(a.view(np.int64)).to(dev)
+    db = torch.from_numpy(b.view(np.int64)).to(dev)
+    be = GpuBackend(mp, plan, dev)
+    comm = TorchComm(host_staging=(world > 1 and not dist.get_backend() == "nccl")) if world > 1 else None
+    job = ShardedMul(plan, rank, be, comm if comm else _SoloComm())
+    for _ in range(args.warmup):
+        job.run(da, db)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        m0, limbs = job.run(da, db)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return {"metric": "limbs/s for new_mpn_mul N×N-bit at 1/2/4/8 MI355X; % HBM roofline",
+            "value": 2 * nl * args.steps / el, "unit": "limbs/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": f"sharded new_mpn_mul depth={depth} w={w} n1=n2={nl}",
+                       "parallelism": f"MFA columns x{world}, 3 all-to-all"}}
+
+
+class _SoloComm:
+    """world == 1: exchanges are local copies."""
+
+    def all_to_all(self, out, inp, out_splits, in_splits):
+        out[: inp.numel()].copy_(inp)
+
+    def all_gather(self, t):
+        return [t]
