@@ -443,12 +443,15 @@ __device__ __forceinline__ i64 rot_digit(const i64 *stage, int j, const Rot &r, 
 template <int U>
 __device__ __forceinline__ void rot_write(const WG &c, const i64 (&x)[2 * U], i64 *stage, int l)
 {
+    typedef long long v2i __attribute__((ext_vector_type(2)));
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         int m = u * c.nt + c.t;
         if (m < l) {
-            stage[2 * m] = x[2 * u];
-            stage[2 * m + 1] = x[2 * u + 1];
+            v2i v;
+            v.x = x[2 * u];
+            v.y = x[2 * u + 1];
+            *(v2i *)(stage + 2 * m) = v;   // one ds_write_b128 per limb
         }
     }
 }
@@ -457,6 +460,40 @@ template <int U>
 __device__ __forceinline__ void rot_read(const WG &c, i64 (&x)[2 * U], const i64 *stage, const Rot &r, int l)
 {
     const int L = 2 * l;
+    if (r.b == 0 && !(r.y & 1)) {
+        // limb-aligned shift (every FFT twiddle when w*NC and w*NR are multiples of 64):
+        // a signed limb permutation, one 16-byte LDS read per limb
+        typedef long long v2i __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int m = u * c.nt + c.t;
+            if (m < l) {
+                int k = 2 * m - r.y;
+                i64 sg = r.sgn;
+                if (k < 0) { k += L; sg = -sg; }
+                const v2i v = *(const v2i *)(stage + k);
+                x[2 * u] = sg * v.x;
+                x[2 * u + 1] = sg * v.y;
+            }
+        }
+        return;
+    }
+    if (r.b == 0) {   // digit-aligned: signed digit permutation
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int m = u * c.nt + c.t;
+            if (m < l) {
+#pragma unroll
+                for (int v = 0; v < 2; ++v) {
+                    int k = 2 * m + v - r.y;
+                    i64 sg = r.sgn;
+                    if (k < 0) { k += L; sg = -sg; }
+                    x[2 * u + v] = sg * stage[k];
+                }
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         int m = u * c.nt + c.t;

@@ -83,7 +83,8 @@ template <int U, int G, typename EF>
 __device__ __forceinline__ void rotate_all(const WG &c, i64 (&x)[G][2 * U], EF efn, u64 N, int l, i64 *stage,
                                            int rb)
 {
-    if (rb >= G) {
+    // U == 1 (l <= 256): all G slots always fit (host guarantees rb >= G); keep one code path
+    if (U == 1 || rb >= G) {
         bool any = false;
 #pragma unroll
         for (int i = 0; i < G; ++i) {
@@ -101,7 +102,7 @@ __device__ __forceinline__ void rotate_all(const WG &c, i64 (&x)[G][2 * U], EF e
             if (e) rot_read<U>(c, x[i], stage + (size_t)i * 2 * l, make_rot(e, N), l);
         }
         __syncthreads();
-    } else {
+    } else if (U != 1) {
 #pragma unroll
         for (int i = 0; i < G; ++i) {
             const u64 e = efn(i);
