@@ -479,7 +479,7 @@ __global__ __launch_bounds__(1024) void k_pointwise(u64 *digA, u64 *cbA, int *to
     sm.stage = nullptr;
     sm.edge = (int *)smem;                       // As/Bs are dead by now
     sm.scr = scr;
-    normalize_store<U, 1>(c, dd, slots, keep, true, st, l, sm);
+    normalize_store<U, 1>(c, dd, slots, keep, false, st, l, sm);  // reduced: the inverse pass folds the carries
 }
 
 // --------------------------------------------------------------------------
@@ -655,7 +655,212 @@ __global__ __launch_bounds__(1024) void k_pw(u64 *digA, u64 *cbA, int *topA, con
     sm.stage = nullptr;
     sm.edge = (int *)smem;
     sm.scr = scr;
-    normalize_store<U, 1>(c, d, slots, keep, true, st, l, sm);
+    normalize_store<U, 1>(c, d, slots, keep, false, st, l, sm);   // reduced: the inverse pass folds the carries
+}
+
+// --------------------------------------------------------------------------
+// k_pwm<U,FT>: the pointwise product on the matrix cores (l % 128 == 0).
+//
+// A big-integer product is a Toeplitz matrix times a vector; split into 32-byte
+// blocks it becomes a GEMM that v_mfma_i32_32x32x32_i8 runs at 32 K-terms per
+// lane-pair per instruction.  With bytes u_i of a, v_j of b (L8 = 8 l of each):
+//   c_m = sum_i u_i v_{m-i},   output block p holds c_{32p + s}, s < 32,
+//   C[s][p] = sum_d sum_t Tq_d[s][t] * vb_{p-d}[t],  Tq_d[s][t] = u_{32d + s - t},
+// i.e. for every block distance d one 32x32 Toeplitz tile of a (A operand) times
+// a sliding window of 32 consecutive 32-byte blocks of b (B operand), accumulated
+// over d in the MFMA accumulator.  The i8 MFMA is signed, so digits are offset
+// binary: s_i = u_i - 128 (= byte ^ 0x80), t_j = v_j - 128, and
+//   c_m = conv(s, t)_m + 128 W(m),  W(m) = sum_{i in win(m)} (u_i + v_i - 128)
+// (win(m) = [max(0, m-L8+1), min(m, L8-1)]), a prefix-sum correction.
+// Negacyclic fold (2^N == -1): output block p and p + NB (NB = l/4 blocks) land
+// in the same lane and register of the two accumulators a wave keeps per "fold
+// tile" (32 output blocks), so digit q (32-bit, X = 2^32) of the residue is
+//   F_q = sum_e 2^(8e) (lo - hi)[row 4q+e] + 128 sum_e 2^(8e) (2 PZ[4q+e] - PZ_tot).
+// |F_q| < 2^57 at l = 4096; the canonical normaliser takes |digit| < 2^62.
+// MFMA operands: A lane (r, h) holds s_{32d + r - 16h - j}, j < 16 (16 bytes of
+// the byte-reversed a at a lane-dependent byte offset: 5 aligned dword reads +
+// v_alignbyte), B lane (c, h) holds t bytes [32(p - d) + 16h, +16) (one aligned
+// ds_read_b128).  Element j of lane half h pairs A and B by the same t = 16h + j,
+// so the hardware's own k order inside a fragment does not matter.
+// C/D map (gfx950, dtype-independent): col = lane & 31, row = (reg & 3) + 8 (reg >> 2)
+// + 4 (lane >> 5): each lane's 4 consecutive rows are the 4 bytes of one digit.
+// Per slot: NB/32 fold tiles x (NB + 32) MFMAs; one workgroup per slot, wave w
+// owns fold tiles w, w + nw, ...; blockDim = 64 min(NB/32, 16), U = l / blockDim.
+// LDS: SR[L8 + 96] (reversed s, 32-byte zero pads) | TB[L8 + 2048] (t, 1 KB
+// zero pads) | PZ[L32 + 1] int | wave sums | normaliser scratch; the digit
+// array DG[L32] i64 reuses SR/TB after the MFMA phase.
+// Reference: new_mpn_mulmod_2expp1 (mul_fft.c:3119) -> MPIR mpn_mulmod_2expp1.
+// --------------------------------------------------------------------------
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+typedef int v16i_t __attribute__((ext_vector_type(16)));
+
+__host__ __device__ inline size_t pwm_lds_bytes(int l, int U, int nw)
+{
+    const size_t L8 = 8 * (size_t)l;
+    size_t b = (L8 + 96) + (L8 + 2048) + ((2 * (size_t)l + 1) * 4 + 15) / 16 * 16 + 64;
+    b += ((size_t)norm_edge_ints(1, U, nw) * sizeof(int) + 15) / 16 * 16;
+    return b + (size_t)norm_scr_u64(1, U, nw) * sizeof(u64);
+}
+
+template <int U, int FT>
+__global__ __launch_bounds__(1024) void k_pwm(u64 *digA, u64 *cbA, int *topA, const u64 *digB, const int *topB,
+                                              int l)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const WG c = wg_ctx();
+    const int L8 = 8 * l, NB = l / 4, L32 = 2 * l;
+    unsigned char *SR = smem;
+    unsigned char *TB = SR + L8 + 96;
+    int *PZ = (int *)(TB + L8 + 2048);
+    int *wsum = PZ + ((L32 + 1) * 4 + 15) / 16 * 4;
+    Lds sm;
+    sm.stage = nullptr;
+    sm.edge = wsum + 16;
+    sm.scr = (u64 *)((unsigned char *)sm.edge + ((size_t)norm_edge_ints(1, U, c.nw) * sizeof(int) + 15) / 16 * 16);
+    Coef st;
+    st.dig = digA;
+    st.cb = cbA;
+    st.top = topA;
+    const long slot = blockIdx.x;
+    const int ta = topA[slot], tb = topB[slot];  // canonical inputs: tops in {0, 1}
+    const u64 *pa = digA + (size_t)slot * l;
+    const u64 *pb = digB + (size_t)slot * l;
+    constexpr u64 X80 = 0x8080808080808080ull;
+
+    u64 amine[U], bmine[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {                      // blockDim * U == l: every thread owns U limbs
+        const int m = u * c.nt + c.t;
+        amine[u] = pa[m];
+        bmine[u] = pb[m];
+    }
+    i64 d[1][2 * U];
+    if (ta | tb) {
+        // 2^N == -1: the product is -b, -a or 1 (MPIR's c flags, mul_fft.c:3250)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int m = u * c.nt + c.t;
+            if (ta && tb) {
+                d[0][2 * u] = (m == 0) ? 1 : 0;
+                d[0][2 * u + 1] = 0;
+            } else {
+                const u64 o = ta ? bmine[u] : amine[u];
+                d[0][2 * u] = -(i64)(o & MPF_M32);
+                d[0][2 * u + 1] = -(i64)(o >> 32);
+            }
+        }
+    } else {
+        // ---- stage the signed digits and the per-dword window sums --------------------
+        for (int i = c.t; i < 8; i += c.nt) ((u32 *)SR)[i] = 0;
+        for (int i = c.t; i < 16; i += c.nt) ((u32 *)(SR + 32 + L8))[i] = 0;
+        for (int i = c.t; i < 256; i += c.nt) {
+            ((u32 *)TB)[i] = 0;
+            ((u32 *)(TB + 1024 + L8))[i] = 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int m = u * c.nt + c.t;
+            const u64 va = amine[u], vb = bmine[u];
+            *(u64 *)(SR + 32 + L8 - 8 - 8 * m) = __builtin_bswap64(va ^ X80);
+            *(u64 *)(TB + 1024 + 8 * m) = vb ^ X80;
+            const int z0 = (int)__builtin_amdgcn_sad_u8((u32)va, 0, 0) + (int)__builtin_amdgcn_sad_u8((u32)vb, 0, 0);
+            const int z1 = (int)__builtin_amdgcn_sad_u8((u32)(va >> 32), 0, 0) +
+                           (int)__builtin_amdgcn_sad_u8((u32)(vb >> 32), 0, 0);
+            PZ[2 * m] = z0 - 512;
+            PZ[2 * m + 1] = z1 - 512;
+        }
+        __syncthreads();
+        // exclusive prefix over the L32 dwords: thread t scans [2U t, 2U t + 2U)
+        {
+            int v[2 * U], run = 0;
+#pragma unroll
+            for (int k = 0; k < 2 * U; ++k) {
+                v[k] = run;
+                run += PZ[2 * U * c.t + k];
+            }
+            int x = run;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(x, o);
+                if (c.lane >= o) x += y;
+            }
+            if (c.lane == 63) wsum[c.wave] = x;
+            __syncthreads();
+            int base = x - run;
+            for (int w = 0; w < c.wave; ++w) base += wsum[w];
+#pragma unroll
+            for (int k = 0; k < 2 * U; ++k) PZ[2 * U * c.t + k] = base + v[k];
+            if (c.t == c.nt - 1) PZ[L32] = base + run;
+        }
+        __syncthreads();
+
+        // ---- MFMA phase ------------------------------------------------------------------
+        const int r = c.lane & 31, h = c.lane >> 5;
+        const int oA = 32 + L8 - 1 - r + 16 * h;          // SR byte of A element j = 0 at d = 0
+        const u32 sh = (u32)(oA & 3);
+        const u32 *Ab = (const u32 *)(SR + (oA & ~3));     // - 8 dwords per d
+        i64 F[FT][4];
+        const i64 PZt = PZ[L32];
+#pragma unroll
+        for (int ft = 0; ft < FT; ++ft) {
+            const int p0 = 32 * (c.wave + ft * c.nw);
+            const v4i_t *Blo = (const v4i_t *)(TB + 32 * (p0 + r + 32) + 16 * h);   // - 2 v4i per d
+            const v4i_t *Bhi = Blo + 2 * NB;
+            v16i_t lo = {}, hi = {};
+            auto afrag = [&](int dd) {
+                const u32 *ap = Ab - 8 * dd;
+                const u32 w0 = ap[0], w1 = ap[1], w2 = ap[2], w3 = ap[3], w4 = ap[4];
+                v4i_t a;
+                a.x = (int)__builtin_amdgcn_alignbyte(w1, w0, sh);
+                a.y = (int)__builtin_amdgcn_alignbyte(w2, w1, sh);
+                a.z = (int)__builtin_amdgcn_alignbyte(w3, w2, sh);
+                a.w = (int)__builtin_amdgcn_alignbyte(w4, w3, sh);
+                return a;
+            };
+            for (int dd = 0; dd <= p0; ++dd)
+                lo = __builtin_amdgcn_mfma_i32_32x32x32_i8(afrag(dd), Blo[-2 * dd], lo, 0, 0, 0);
+            for (int dd = p0 + 1; dd <= p0 + 31; ++dd) {
+                const v4i_t a = afrag(dd);
+                lo = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, Blo[-2 * dd], lo, 0, 0, 0);
+                hi = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, Bhi[-2 * dd], hi, 0, 0, 0);
+            }
+            for (int dd = p0 + 32; dd <= NB; ++dd)
+                hi = __builtin_amdgcn_mfma_i32_32x32x32_i8(afrag(dd), Bhi[-2 * dd], hi, 0, 0, 0);
+            // fold + window-sum correction: digit q = 8 p + 2 g + h of the residue
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int q = 8 * (p0 + r) + 2 * g + h;
+                const u32 u4 = __builtin_bswap32(*(const u32 *)(SR + 28 + L8 - 4 * q)) ^ 0x80808080u;
+                const u32 v4 = *(const u32 *)(TB + 1024 + 4 * q) ^ 0x80808080u;
+                i64 run = PZ[q], cz = 0, acc = 0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    run += (i64)((u4 >> (8 * e)) & 255) + (i64)((v4 >> (8 * e)) & 255) - 128;
+                    cz += run << (8 * e);
+                    acc += ((i64)lo[4 * g + e] - (i64)hi[4 * g + e]) << (8 * e);
+                }
+                F[ft][g] = acc + 128 * (2 * cz - PZt * (i64)0x01010101);
+            }
+        }
+        __syncthreads();                                   // SR/TB dead: digits go to DG
+        i64 *DG = (i64 *)smem;
+#pragma unroll
+        for (int ft = 0; ft < FT; ++ft) {
+            const int p0 = 32 * (c.wave + ft * c.nw);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) DG[8 * (p0 + r) + 2 * g + h] = F[ft][g];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int m = u * c.nt + c.t;
+            d[0][2 * u] = DG[2 * m];
+            d[0][2 * u + 1] = DG[2 * m + 1];
+        }
+    }
+    long slots[1] = {slot};
+    bool keep[1] = {true};
+    normalize_store<U, 1>(c, d, slots, keep, false, st, l, sm);   // reduced: the inverse pass folds the carries
 }
 
 // --------------------------------------------------------------------------

@@ -145,6 +145,14 @@ static pass_fn get_pass(int U, int logg, int dir)
     return nullptr;
 }
 
+// pointwise kernel choice: 0 = int8 MFMA (k_pwm, l % 128 == 0), 1 = VALU MAC (k_pw).
+// MPFFT_POINTWISE=valu forces the VALU kernel (A/B parity and timing).
+static int pw_kind()
+{
+    const char *e = getenv("MPFFT_POINTWISE");
+    return (e && !strcmp(e, "valu")) ? 1 : 0;
+}
+
 // dynamic LDS above 64 KiB must be opted into per kernel (gfx950 has 160 KiB per CU)
 static void allow_lds(const void *f, size_t bytes)
 {
@@ -311,6 +319,21 @@ struct Exec {
     {
         const long cnt = (long)rcount * P.NC;
         if (cnt == 0) return MPFFT_OK;
+        if (P.l % 128 == 0 && pw_kind() == 0) {   // int8 MFMA Toeplitz product
+            const int nw = std::min((int)P.l / 128, 16);
+            const int tpb = 64 * nw;
+            const int U = (int)P.l / tpb;
+            const size_t lds = pwm_lds_bytes((int)P.l, U, nw);
+            void (*f)(u64 *, u64 *, int *, const u64 *, const int *, int) = nullptr;
+            if (U == 2) f = k_pwm<2, 1>;
+            else if (U == 4) f = k_pwm<4, 2>;
+            else return MPFFT_EUNSUPPORTED;
+            allow_lds((const void *)f, lds);
+            hipLaunchKernelGGL(f, dim3((unsigned)cnt), dim3(tpb), lds, s, row.dig[0], row.cb[0], row.top[0],
+                               (const u64 *)row.dig[1], (const int *)row.top[1], (int)P.l);
+            HIPCHK(hipGetLastError());
+            return MPFFT_OK;
+        }
         if (P.l % 2 == 0 && P.l >= 32) {   // register-blocked kernel: R columns per thread
             const int R = P.l >= 2048 ? 8 : 4;
             const int L = 2 * (int)P.l;

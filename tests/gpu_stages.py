@@ -6,7 +6,7 @@ Stage specs:
   forward  slot p*NC + q = X_{revbin(p) + NR revbin(q)} mod 2^N + 1, canonical,
            X_k = sum_j x_j 2^(w j k) (a3 output spec, up to the reference's two
            revbin permutations which this build never performs), p < T/NC
-  pointwise slot = XA * XB mod 2^N + 1, canonical                      (a20)
+  pointwise slot = XA * XB mod 2^N + 1, reduced form (limbs + carry masks) (a20)
   inverse  slot j = c_j = sum_i a_i b_(j-i), exact, j < trunc           (a13, a21)
   combine  r = i1 * i2                                                  (a22)
 """
@@ -32,8 +32,30 @@ def _slots(mp, ws, n1, n2, depth, w, which):
     return dig.cpu().numpy().view(np.uint64), top.cpu().numpy().astype(np.int64)
 
 
+def _cbs(mp, ws, n1, n2, depth, w, which):
+    """carry masks of the reduced form: word 2W (2W+1) bit k = limb 64W+k carries +1 (-1)"""
+    lay = mp.workspace_layout(n1, n2, depth, w)
+    off, cbw, slots = lay["cbA" if which == 0 else "cbB"], lay["cbw"], lay["slots"]
+    u8 = ws.view(__import__("torch").uint8)
+    return u8[off:off + slots * cbw * 8].view(__import__("torch").int64).view(slots, cbw).cpu().numpy().view(np.uint64)
+
+
 def _val(dig, top, s, N):
     return to_int(dig[s]) + int(top[s]) * (1 << N)
+
+
+def _val_reduced(dig, top, cb, s, N):
+    """value of a reduced-form slot: limbs + carries (limb m's carry lands at 2^(64(m+1)),
+    limb l-1's at 2^N) + top 2^N"""
+    v = _val(dig, top, s, N)
+    for W in range(len(cb[s]) // 2):
+        pos, neg = int(cb[s][2 * W]), int(cb[s][2 * W + 1])
+        for k in range(64):
+            if (pos >> k) & 1:
+                v += 1 << (64 * (64 * W + k + 1))
+            if (neg >> k) & 1:
+                v -= 1 << (64 * (64 * W + k + 1))
+    return v
 
 
 def _canonical(dig, top, s):
@@ -86,10 +108,11 @@ def run_stages(mp, depth, w, a, b, dev="cuda:0", check=("fwd", "pw", "inv", "com
     torch.cuda.synchronize()
     if "pw" in check:
         dig, top = _slots(mp, ws, n1, n2, depth, w, 0)
+        cbA = _cbs(mp, ws, n1, n2, depth, w, 0)
         for s in range(T):
             want = XA[s] * XB[s] % p
-            got = _val(dig, top, s, N)
-            if not _canonical(dig, top, s) or got != want:
+            got = _val_reduced(dig, top, cbA, s, N) % p    # reduced form (what the inverse pass loads)
+            if got != want:
                 fails.append(f"pointwise slot {s}: got {got:x} (top {top[s]}) want {want:x}")
                 if len(fails) > 8:
                     return fails

@@ -30,9 +30,12 @@ def torch_dev():
 STAGE_SHAPES = [(6, 1, 3, 2), (6, 1, 1, 1), (7, 1, 5, 4), (7, 3, 13, 2), (8, 2, 30, 25), (8, 4, 60, 50),
                 (9, 1, 30, 31), (10, 3, 300, 200), (11, 1, 1000, 1000), (5, 2, 2, 1), (4, 4, 1, 1),
                 (3, 8, 1, 1), (2, 16, 1, 1)]
+# coefficient sizes l = 128 ... 4096 limbs: the int8-MFMA pointwise (k_pwm<2,1>, k_pwm<4,2>)
+MFMA_SHAPES = [(9, 16, 2000, 1500), (8, 64, 3000, 2000), (7, 256, 4000, 3000), (6, 1024, 6000, 5000),
+               (5, 4096, 8000, 8000), (6, 4096, 20000, 20000)]
 
 
-@pytest.mark.parametrize("depth,w,n1,n2", STAGE_SHAPES)
+@pytest.mark.parametrize("depth,w,n1,n2", STAGE_SHAPES + MFMA_SHAPES)
 def test_stages_exact(mp, torch_dev, depth, w, n1, n2):
     from gpu_stages import run_stages
     if not valid_shape(depth, w, n1, n2):
@@ -94,6 +97,65 @@ def test_adversarial_inputs(mp, oracle):
                 continue
             got = mp.mul(a, b, depth, w)
             assert (got == oracle.gmp_mul(a, b)).all(), (depth, w, len(a), len(b))
+
+
+def _pattern(kind, l, N, rng):
+    """canonical residues (limbs, top) that stress the pointwise kernels"""
+    if kind == 1:
+        return 0, 1                                          # 2^N == -1
+    v = {0: rng.getrandbits(N), 2: (1 << N) - 1, 3: 0, 4: 1,
+         5: int.from_bytes(b"\x80" * (8 * l), "little"), 6: int.from_bytes(b"\x7f" * (8 * l), "little"),
+         7: (1 << N) - 1 - rng.getrandbits(64)}[kind]
+    return v, 0
+
+
+@pytest.mark.parametrize("kind", ["mfma", "valu"])
+@pytest.mark.parametrize("depth,w", [(11, 1), (9, 16), (8, 64), (7, 256), (6, 1024), (6, 4096)])
+def test_pointwise_direct(mp, torch_dev, kind, depth, w):
+    """The pointwise stage alone on hand-placed canonical inputs (every pair of the
+    special values 0, 1, 2^N - 1, 2^N, 0x80.. and 0x7f.. bytes, random), for the
+    int8-MFMA kernel (l % 128 == 0) and the VALU kernel (MPFFT_POINTWISE=valu)."""
+    import torch
+    from gpu_stages import _cbs, _val_reduced
+    mx = max_limbs(depth, w)
+    n1 = n2 = mx
+    P = mp.plan_info(n1, n2, depth, w)
+    l, T, N = P["l"], P["trunc"], P["n"] * w
+    p = (1 << N) + 1
+    rng = random.Random(depth * 1000 + w)
+    ws = mp.alloc_workspace(n1, n2, depth, w, torch_dev)
+    ws.fill_(0)
+    digA, topA, digB, topB = mp.workspace_views(ws, n1, n2, depth, w)
+    want = []
+    host = {k: (np.zeros((T, l), np.uint64), np.zeros(T, np.int32)) for k in "AB"}
+    for sl in range(T):
+        va, ta = _pattern(sl % 8, l, N, rng)
+        vb, tb = _pattern((sl // 8) % 8, l, N, rng)
+        for k, v, t in (("A", va, ta), ("B", vb, tb)):
+            host[k][0][sl] = np.frombuffer(v.to_bytes(8 * l, "little"), dtype=np.uint64)
+            host[k][1][sl] = t
+        want.append((va + ta * (1 << N)) * (vb + tb * (1 << N)) % p)
+    for k, dig, top in (("A", digA, topA), ("B", digB, topB)):
+        dig[:T] = torch.from_numpy(host[k][0].view(np.int64)).to(torch_dev)
+        top[:T] = torch.from_numpy(host[k][1]).to(torch_dev)
+    da = torch.zeros(n1, dtype=torch.int64, device=torch_dev)
+    db = torch.zeros(n2, dtype=torch.int64, device=torch_dev)
+    dr = torch.zeros(n1 + n2, dtype=torch.int64, device=torch_dev)
+    old = os.environ.get("MPFFT_POINTWISE")
+    os.environ["MPFFT_POINTWISE"] = kind
+    try:
+        mp.stage(mp.STAGE_POINTWISE, da, db, dr, n1, n2, depth, w, ws)
+        torch.cuda.synchronize()
+    finally:
+        if old is None:
+            del os.environ["MPFFT_POINTWISE"]
+        else:
+            os.environ["MPFFT_POINTWISE"] = old
+    dig = digA.cpu().numpy().view(np.uint64)
+    top = topA.cpu().numpy().astype(np.int64)
+    cb = _cbs(mp, ws, n1, n2, depth, w, 0)
+    bad = [sl for sl in range(T) if _val_reduced(dig, top, cb, sl, N) % p != want[sl]]
+    assert not bad, f"{len(bad)} of {T} slots wrong, first {bad[:8]}"
 
 
 def test_coefficient_equal_2N(mp, oracle):
