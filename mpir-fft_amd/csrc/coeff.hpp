@@ -27,6 +27,7 @@ typedef int64_t i64;
 typedef uint32_t u32;
 typedef __int128 i128;
 typedef unsigned __int128 u128;
+typedef uint8_t u8;
 
 #define MPF_M32 0xFFFFFFFFull
 #define MPF_MAXL 0xFFFFFFFFFFFFFFFFull

@@ -26,13 +26,25 @@
 #include <string.h>
 #include <mutex>
 
-typedef uint8_t u8;
 #include "kernels.hpp"
+#include "combine.hpp"
+#include "wdispatch.hpp"
 #include "../../include/mpfft.h"
 
 // ---------------------------------------------------------------------------
 // parameters (mul_fft.c:3193-3203)
 // ---------------------------------------------------------------------------
+// wave kernels for coefficients of l limbs: U = ceil(l / 64) limbs per lane, full rows when l == 64 U
+static WvFns wv_fns(int U, bool full)
+{
+    switch (U) {
+    case 1: return full ? wv_fns_u1_1() : wv_fns_u1_0();
+    case 2: return full ? wv_fns_u2_1() : wv_fns_u2_0();
+    case 3: return full ? wv_fns_u3_1() : wv_fns_u3_0();
+    default: return full ? wv_fns_u4_1() : wv_fns_u4_0();
+    }
+}
+
 struct Plan {
     long n1, n2;
     int depth;
@@ -43,6 +55,11 @@ struct Plan {
     int lbC, lbR;
     long j1, j2, trunc, Tr, len, total;
     int U, tpb, maxlogg;
+    bool wave;          // wave-owned coefficient kernels (wkernels.hpp), l <= 512
+    int wU;             // their limbs per lane
+    bool wfull;         // l == 64 wU
+    bool fuse_scale;    // scaling fused into the last inverse column pass (no truncation)
+    bool lds;           // LDS-resident radix-2^5 passes (lkernels.hpp)
     size_t slots;       // allocated slots per operand
     size_t off_digA, off_topA, off_cbA, off_digB, off_topB, off_cbB, off_lo, off_hi, off_bg, off_bp, off_bc, bytes;
     long nblk;
@@ -88,6 +105,24 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
     p->tpb = (int)tpb;
     p->U = Up;
     p->maxlogg = Up == 1 ? 4 : Up == 2 ? 2 : 1;   // G*U <= 8 keeps U >= 2 passes spill-free
+    {
+        const char *e = getenv("MPFFT_WAVE");
+        p->wave = p->l <= 256 && !(e && !strcmp(e, "0"));
+    }
+    if (p->wave) {
+        p->wU = (int)((p->l + 63) / 64);
+        p->wfull = p->l == 64L * p->wU;
+        p->maxlogg = wv_fns(p->wU, p->wfull).maxlogg;
+        const char *e = getenv("MPFFT_WLOGG");
+        if (e && atoi(e) >= 1 && atoi(e) <= p->maxlogg) p->maxlogg = atoi(e);
+        p->fuse_scale = p->Tr == p->NR;
+        const char *el = getenv("MPFFT_LDS");
+        p->lds = !(el && !strcmp(el, "0"));
+        if (p->lds) {
+            p->maxlogg = LP_MAXLOGG;
+            if (e && atoi(e) >= 1 && atoi(e) <= LP_MAXLOGG) p->maxlogg = atoi(e);
+        }
+    }
     p->slots = (size_t)2 * p->n;
     size_t o = 0;
     const size_t dig = p->slots * p->l * 8, top = align_up(p->slots * 4, 256);
@@ -134,6 +169,8 @@ static pass_fn pick_pass(int logg, int dir)
     }
     return nullptr;
 }
+
+static size_t wpass_lds(int U, int G, int l) { return (size_t)WPB * wv_stage_slots(G, U) * 16 * (size_t)l; }
 
 static pass_fn get_pass(int U, int logg, int dir)
 {
@@ -212,6 +249,33 @@ struct Exec {
 
     int pass(PassArgs a, int logg, int dir, int nops)
     {
+        if (P.wave && P.lds) {
+            pass_fn f = wv_fns(P.wU, P.wfull).lpass(logg, dir);
+            if (!f) return MPFFT_EUNSUPPORTED;
+            const size_t lds = ((size_t)16 * P.l) << logg;
+            allow_lds((const void *)f, lds);
+            a.ngroups = 1 << (a.lbM - logg);
+            dim3 grid((unsigned)((long)a.nsub * a.ngroups), (unsigned)nops);
+            hipLaunchKernelGGL(f, grid, dim3(32 << logg), lds, s, a);
+            HIPCHK(hipGetLastError());
+            return MPFFT_OK;
+        }
+        if (P.wave) {
+            {
+                const char *e = getenv("MPFFT_ABLATE");
+                a.ablate = e ? atoi(e) : 0;
+            }
+            pass_fn f = wv_fns(P.wU, P.wfull).pass(logg, dir);
+            if (!f) return MPFFT_EUNSUPPORTED;
+            const size_t lds = wpass_lds(P.wU, 1 << logg, (int)P.l);
+            allow_lds((const void *)f, lds);
+            a.ngroups = 1 << (a.lbM - logg);
+            const long waves = (long)a.nsub * a.ngroups;
+            dim3 grid((unsigned)((waves + WPB - 1) / WPB), (unsigned)nops);
+            hipLaunchKernelGGL(f, grid, dim3(64 * WPB), lds, s, a);
+            HIPCHK(hipGetLastError());
+            return MPFFT_OK;
+        }
         pass_fn f = get_pass(P.U, logg, dir);
         if (!f) return MPFFT_EUNSUPPORTED;
         const int G = 1 << logg;
@@ -390,6 +454,10 @@ struct Exec {
             a.pos_off = (int)off;
             a.zero_from = (int)m;
             a.need = (int)m;
+            if (P.fuse_scale && hi - k == 0 && m == P.NR) {   // the whole column inverse is this block
+                a.scale_e = 2 * P.N - (u64)(P.depth + 1);
+                a.canon = 1;
+            }
             int rc = pass(a, k, 1, 1);
             if (rc) return rc;
             hi -= k;
@@ -414,6 +482,15 @@ struct Exec {
         a.i0 = (int)i0;
         a.cnt = (int)cnt;
         a.rho = rho;
+        if (P.wave) {
+            void (*f)(PairArgs) = wv_fns(P.wU, P.wfull).pair;
+            const size_t lds = (size_t)WPB * 16 * P.l;
+            allow_lds((const void *)f, lds);
+            const long waves = cnt * ccount;
+            hipLaunchKernelGGL(f, dim3((unsigned)((waves + WPB - 1) / WPB)), dim3(64 * WPB), lds, s, a);
+            HIPCHK(hipGetLastError());
+            return MPFFT_OK;
+        }
         const size_t lds = lds_bytes((int)P.l, 2, 2, P.U, nw);
         void (*f)(PairArgs) = nullptr;
         switch (P.U) {
@@ -467,6 +544,16 @@ struct Exec {
     int scale()
     {
         const long cnt = (long)P.Tr * ccount;
+        if (P.fuse_scale) return MPFFT_OK;   // done by the last inverse column pass
+        if (P.wave) {
+            wv_scale_fn f = wv_fns(P.wU, P.wfull).scale;
+            const size_t lds = (size_t)WPB * 16 * P.l;
+            allow_lds((const void *)f, lds);
+            hipLaunchKernelGGL(f, dim3((unsigned)((cnt + WPB - 1) / WPB)), dim3(64 * WPB), lds, s, col.dig[0],
+                               col.cb[0], col.top[0], (int)P.l, P.N, 2 * P.N - (u64)(P.depth + 1), cnt);
+            HIPCHK(hipGetLastError());
+            return MPFFT_OK;
+        }
         const size_t lds = lds_bytes((int)P.l, 1, 1, P.U, nw);
         void (*f)(u64 *, u64 *, int *, int, u64, u64) = nullptr;
         switch (P.U) {
