@@ -42,7 +42,15 @@ CONFIGS = {
 SEED1, SEED2 = 0x1001, 0x2002
 
 STAGE_NAMES = ["fwd_columns", "fwd_rows", "pointwise", "inv_rows", "inv_columns", "scale", "combine"]
-STAGE_KERNEL = {"pointwise": "k_pw<4> (register-blocked asm MAC)", "scale": "k_scale"}
+STAGE_KERNEL = {"pointwise": "k_pwm (negacyclic products on v_mfma_i32_32x32x32_i8)", "scale": "k_scale",
+                "combine": "k_comb_sum + k_carry_*"}
+I8_MFMA_PEAK = 5.0e15      # int8 ops/s dense: 2x the 2.5 PF BF16 rate per clock (MI355X_MICROARCH.md)
+
+
+def pointwise_ops(P):
+    """Algorithmic int8 ops of one pointwise launch: T products of two 8l-byte numbers,
+    (8l)^2 byte MACs each, 2 ops per MAC (the schoolbook the int8 MFMA path executes)."""
+    return P["trunc"] * 2 * (8 * P["l"]) ** 2
 
 
 def stage_bytes(P, name, n1, n2):
@@ -138,6 +146,9 @@ def main():
     ws = mp.alloc_workspace(n1, n2, depth, w, dev)
     stream = torch.cuda.Stream(device=dev)
 
+    def step_full():
+        mp.mul_device(dr, da, n1, db, n2, depth, w, ws, stream=stream)
+
     def step(events=None):
         for si, _ in enumerate(STAGE_NAMES):
             if events is not None:
@@ -148,16 +159,17 @@ def main():
 
     with torch.cuda.stream(stream):
         for _ in range(args.warmup):
-            step()
+            step_full()
     torch.cuda.synchronize(dev)
 
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(STAGE_NAMES) + 1)] for _ in range(args.steps)]
+    # timed region: K whole multiplies, one library call each (no per-stage events:
+    # an event record between two kernels costs ~5 us of idle GPU)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(ev[k])
+        step_full()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -167,6 +179,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
+    # stage breakdown: the same K multiplies again, stage by stage, with HIP events
+    # recorded on the library's stream around every stage
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(STAGE_NAMES) + 1)] for _ in range(args.steps)]
+    torch.cuda.synchronize(dev)
+    for k in range(args.steps):
+        step(ev[k])
+    torch.cuda.synchronize(dev)
     stage_ms = np.zeros(len(STAGE_NAMES))
     for k in range(args.steps):
         for si in range(len(STAGE_NAMES)):
@@ -191,6 +210,15 @@ def main():
     dname = STAGE_NAMES[dom]
     dbytes = stage_bytes(P, dname, n1, n2)
     achieved = dbytes / (stage_ms[dom] * 1e-3)
+    if dname == "pointwise" and P["l"] % 128 == 0:     # matrix-core kernel: priced against the int8 MFMA peak
+        ops = pointwise_ops(P)
+        roof = {"bound": "mfma", "achieved": ops / (stage_ms[dom] * 1e-3) / 1e12, "peak": I8_MFMA_PEAK / 1e12,
+                "unit": "TFLOP/s", "op_type": "int8 MAC ops (2 per MAC), TOP/s",
+                "frac": ops / (stage_ms[dom] * 1e-3) / I8_MFMA_PEAK, "alg_ops_per_launch": ops,
+                "hbm_achieved_GBps": achieved / 1e9, "alg_bytes_per_launch": dbytes}
+    else:
+        roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK, "alg_bytes_per_launch": dbytes}
     pmc = pmc_traffic(args.config)
     traffic = None
     if pmc and pmc.get("stage") == dname:
@@ -213,13 +241,12 @@ def main():
         "config": {"workload": f"{args.config}: new_mpn_mul depth={depth} w={w} n1=n2={nl} limbs "
                                f"(l={P['l']} limbs/coeff, NC x NR = {P['NC']} x {P['NR']}, trunc={P['trunc']})",
                    "parallelism": f"replicas x{world}" if world > 1 else "single"},
-        "roofline": {"bound": "hbm", "kernel": STAGE_KERNEL.get(dname, "k_pass (" + dname + ")"),
-                     "stage": dname, "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK, "traffic": traffic,
-                     "alg_bytes_per_launch": dbytes, "avg_ms": float(stage_ms[dom])},
+        "roofline": dict(roof, kernel=STAGE_KERNEL.get(dname, "k_lpass (" + dname + ")"), stage=dname,
+                         traffic=traffic, avg_ms=float(stage_ms[dom])),
         "pipeline": {"device_ms": dev_ms, "b_alg_bytes": balg,
                      "hbm_frac_b_alg": balg / (dev_ms * 1e-3) / HBM_PEAK},
         "stages_ms": {n: float(t) for n, t in zip(STAGE_NAMES, stage_ms)},
+        "stage_timing": "separate K-multiply pass after the timed region, HIP events per stage on the library stream",
         "exact": exact,
     }
     if world == 1 and not args.no_cpu_baseline:
