@@ -183,3 +183,150 @@ __global__ __launch_bounds__(256) void k_carry_apply(const u64 *lo64, const u32 
         (void)pk;
     }
 }
+
+// --------------------------------------------------------------------------
+// k_combine1: the whole single-GPU combine in one launch.  Block b owns output limbs
+// [b CB_LIMBS, (b+1) CB_LIMBS): it sums the coefficient windows of its limbs (coalesced,
+// limb m = base + k 256 + t), resolves its carries locally, and gets its carry-in by a
+// decoupled look-back over the blocks before it (flags in `st`, zeroed before the
+// launch; workgroups are dispatched in blockIdx order, so every predecessor is resident or done).
+// The flag is the whole message (no data published beside it), so relaxed agent-scope
+// atomics suffice: release/acquire would write back / invalidate the XCD's L2 per block.
+// Block flag: 0 not ready, 1 aggregate generates, 2 aggregate propagates, 3 aggregate
+// kills, 4 / 5 inclusive carry-out 0 / 1.
+// --------------------------------------------------------------------------
+#define CB_V 1
+#define CB_LIMBS (256 * CB_V)
+
+// floor(x / d) for x < 2^52: double quotient, then an exact integer fix-up
+__device__ __forceinline__ long udiv_exact(u64 x, u64 d)
+{
+    long q = (long)((double)x / (double)d);
+    while ((u64)q * d > x) --q;
+    while ((u64)(q + 1) * d <= x) ++q;
+    return q;
+}
+
+// coef_ptr for a power-of-two NC (always: NC = 2^floor(depth/2)) and no halo
+__device__ __forceinline__ const u64 *coef_ptr2(const CombArgs &a, long k)
+{
+    const int lg = __builtin_ctz((unsigned)a.NC);
+    const long p = (k >> lg) - a.r0;
+    const int cc = (int)(k & (a.NC - 1));
+    const long slot = (long)(cc >> a.cbb) * a.cbs + p * a.ccb + (cc & (a.ccb - 1));
+    return a.dig + (size_t)slot * a.l;
+}
+
+__device__ __forceinline__ void comb_limb(const CombArgs &a, long m, u64 *lo, u32 *hi)
+{
+    const u64 P = (u64)m * 64;
+    long klo = (P >= a.N) ? udiv_exact(P - a.N, a.bits1) : 0;
+    long khi = udiv_exact(P + 63, a.bits1);
+    if (khi > a.len - 1) khi = a.len - 1;
+    u64 slo = 0;
+    u32 shi = 0;
+    for (long k = klo; k <= khi; ++k) {
+        const u64 st = (u64)k * a.bits1;
+        const u64 *cp = coef_ptr2(a, k);
+        u64 v;
+        if (st > P) {
+            v = cp[0] << (st - P);
+        } else {
+            const u64 o = P - st;
+            const long q = (long)(o >> 6);
+            const int s = (int)(o & 63);
+            const u64 w0 = (q < a.l) ? cp[q] : 0;
+            const u64 w1 = (s && q + 1 < a.l) ? cp[q + 1] : 0;
+            v = s ? (w0 >> s) | (w1 << (64 - s)) : w0;
+        }
+        u64 t;
+        shi += add_ovf(slo, v, &t);
+        slo = t;
+    }
+    *lo = slo;
+    *hi = shi;
+}
+
+__global__ __launch_bounds__(256) void k_combine1(CombArgs a, u64 *r, u32 *st)
+{
+    __shared__ u64 L[CB_LIMBS];
+    __shared__ u32 H[CB_LIMBS + 1];
+    __shared__ u64 scr[64];
+    __shared__ u32 sh_cin;
+    const WG c = wg_ctx();
+    const long total = a.mcount;
+        // in-order workgroup dispatch: every block below b is resident or done
+    const long b = blockIdx.x;
+    const long base = b * CB_LIMBS;
+    // window sums: lo of limb base + i -> L[i], its carry (hi) -> H[i + 1]
+#pragma unroll
+    for (int k = 0; k < CB_V; ++k) {
+        const int i = k * 256 + c.t;
+        const long m = base + i;
+        u64 lo = 0;
+        u32 hi = 0;
+        if (m < total) comb_limb(a, m, &lo, &hi);
+        L[i] = lo;
+        H[i + 1] = hi;
+    }
+    if (c.t == 0) {
+        u64 lo = 0;
+        u32 hi = 0;
+        if (base > 0) comb_limb(a, base - 1, &lo, &hi);
+        H[0] = hi;
+    }
+    __syncthreads();
+    // thread t: limbs base + t V .. + V - 1, value v = L + H (H carries the limb below's overflow)
+    u64 v[CB_V];
+    u32 g = 0, p = 0;
+    bool G = false, Pa = true;
+#pragma unroll
+    for (int k = 0; k < CB_V; ++k) {
+        const int i = c.t * CB_V + k;
+        const bool gk = add_ovf(L[i], (u64)H[i], &v[k]);
+        const bool pk = v[k] == MPF_MAXL;
+        g |= (u32)gk << k;
+        p |= (u32)pk << k;
+        G = gk || (pk && G);
+        Pa = Pa && pk;
+    }
+    u32 co0;
+    wg_scan<1>(c, G, Pa, 0, &co0, scr);
+    const bool allp = __syncthreads_and(Pa);
+    // look-back (thread 0)
+    if (c.t == 0) {
+        u32 cin = 0;
+        if (b == 0) {
+            __hip_atomic_store(&st[0], 4u + co0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            const u32 agg = co0 ? 1u : (allp ? 2u : 3u);
+            if (agg != 2u) __hip_atomic_store(&st[b], agg == 1u ? 5u : 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else __hip_atomic_store(&st[b], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (long j = b - 1;; --j) {
+                u32 f;
+                while ((f = __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u)
+                    __builtin_amdgcn_s_sleep(1);
+                if (f >= 4u) { cin = f - 4u; break; }
+                if (f == 1u) { cin = 1; break; }
+                if (f == 3u) { cin = 0; break; }
+            }
+            if (agg == 2u) __hip_atomic_store(&st[b], 4u + cin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        sh_cin = cin;
+    }
+    __syncthreads();
+    u32 co;
+    const u32 ci = wg_scan<1>(c, G, Pa, sh_cin, &co, scr);
+    bool run = ci & 1;
+#pragma unroll
+    for (int k = 0; k < CB_V; ++k) {
+        L[c.t * CB_V + k] = v[k] + (run ? 1 : 0);
+        run = ((g >> k) & 1) || (((p >> k) & 1) && run);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < CB_V; ++k) {
+        const long m = base + k * 256 + c.t;
+        if (m < total) r[m] = L[k * 256 + c.t];
+    }
+}

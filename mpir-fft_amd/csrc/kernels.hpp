@@ -865,3 +865,203 @@ __global__ __launch_bounds__(1024) void k_pwm(u64 *digA, u64 *cbA, int *topA, co
     normalize_store<U, 1>(c, d, slots, keep, false, st, l, sm);   // reduced: the inverse pass folds the carries
 }
 
+
+// --------------------------------------------------------------------------
+// k_pwm2<U,T,D>: k_pwm with the MFMA operands register-blocked to cut LDS traffic.
+// k_pwm reads one Toeplitz A fragment (5 dwords/lane) and one or two B fragments
+// (16 B/lane) per MFMA, so it is bound by LDS bandwidth, not by the matrix cores.
+// Here a wave owns T consecutive fold tiles p0_f = P0 + 32 f and walks the block
+// distances dd in chains dd = k + 32 j (k < 32): for D consecutive j it loads the D
+// A fragments A(k + 32 j) once and the B fragments by m = f - jj, since tile f at
+// dd = k + 32 (j0 + jj) reads block P0 + r + 32 - k + 32 m (+ NB for hi) -- so T D
+// lo MFMAs (and T D hi) need D A loads and T + D - 1 B loads each for lo and hi.
+// Validity (which MFMAs k_pwm issues): lo iff dd <= p0_f + 31, hi iff p0_f + 1 <= dd
+// <= NB; both depend on m only (plus dd <= NB on jj), and are wave-uniform.
+// Same digit math, LDS layout and epilogue as k_pwm.  blockDim = 64 nw with
+// nw T = NB / 32 fold tiles, U = l / blockDim.
+// --------------------------------------------------------------------------
+template <int U, int T, int D>
+__global__ __launch_bounds__(D >= 4 ? 512 : 1024) void k_pwm2(u64 *digA, u64 *cbA, int *topA, const u64 *digB, const int *topB,
+                                               int l, int ablate)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const WG c = wg_ctx();
+    const int L8 = 8 * l, NB = l / 4, L32 = 2 * l;
+    unsigned char *SR = smem;
+    unsigned char *TB = SR + L8 + 96;
+    int *PZ = (int *)(TB + L8 + 2048);
+    int *wsum = PZ + ((L32 + 1) * 4 + 15) / 16 * 4;
+    Lds sm;
+    sm.stage = nullptr;
+    sm.edge = wsum + 16;
+    sm.scr = (u64 *)((unsigned char *)sm.edge + ((size_t)norm_edge_ints(1, U, c.nw) * sizeof(int) + 15) / 16 * 16);
+    Coef st;
+    st.dig = digA;
+    st.cb = cbA;
+    st.top = topA;
+    const long slot = blockIdx.x;
+    const int ta = topA[slot], tb = topB[slot];
+    const u64 *pa = digA + (size_t)slot * l;
+    const u64 *pb = digB + (size_t)slot * l;
+    constexpr u64 X80 = 0x8080808080808080ull;
+
+    u64 amine[U], bmine[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int m = u * c.nt + c.t;
+        amine[u] = pa[m];
+        bmine[u] = pb[m];
+    }
+    i64 d[1][2 * U];
+    if (ta | tb) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int m = u * c.nt + c.t;
+            if (ta && tb) {
+                d[0][2 * u] = (m == 0) ? 1 : 0;
+                d[0][2 * u + 1] = 0;
+            } else {
+                const u64 o = ta ? bmine[u] : amine[u];
+                d[0][2 * u] = -(i64)(o & MPF_M32);
+                d[0][2 * u + 1] = -(i64)(o >> 32);
+            }
+        }
+    } else {
+        for (int i = c.t; i < 8; i += c.nt) ((u32 *)SR)[i] = 0;
+        for (int i = c.t; i < 16; i += c.nt) ((u32 *)(SR + 32 + L8))[i] = 0;
+        for (int i = c.t; i < 256; i += c.nt) {
+            ((u32 *)TB)[i] = 0;
+            ((u32 *)(TB + 1024 + L8))[i] = 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int m = u * c.nt + c.t;
+            const u64 va = amine[u], vb = bmine[u];
+            *(u64 *)(SR + 32 + L8 - 8 - 8 * m) = __builtin_bswap64(va ^ X80);
+            *(u64 *)(TB + 1024 + 8 * m) = vb ^ X80;
+            const int z0 = (int)__builtin_amdgcn_sad_u8((u32)va, 0, 0) + (int)__builtin_amdgcn_sad_u8((u32)vb, 0, 0);
+            const int z1 = (int)__builtin_amdgcn_sad_u8((u32)(va >> 32), 0, 0) +
+                           (int)__builtin_amdgcn_sad_u8((u32)(vb >> 32), 0, 0);
+            PZ[2 * m] = z0 - 512;
+            PZ[2 * m + 1] = z1 - 512;
+        }
+        __syncthreads();
+        {
+            int v[2 * U], run = 0;
+#pragma unroll
+            for (int k = 0; k < 2 * U; ++k) {
+                v[k] = run;
+                run += PZ[2 * U * c.t + k];
+            }
+            int x = run;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(x, o);
+                if (c.lane >= o) x += y;
+            }
+            if (c.lane == 63) wsum[c.wave] = x;
+            __syncthreads();
+            int base = x - run;
+            for (int w = 0; w < c.wave; ++w) base += wsum[w];
+#pragma unroll
+            for (int k = 0; k < 2 * U; ++k) PZ[2 * U * c.t + k] = base + v[k];
+            if (c.t == c.nt - 1) PZ[L32] = base + run;
+        }
+        __syncthreads();
+
+        // ---- MFMA phase: T tiles x chains of D distances ---------------------------------
+        const int r = c.lane & 31, h = c.lane >> 5;
+        const int oA = 32 + L8 - 1 - r + 16 * h;
+        const u32 sh = (u32)(oA & 3);
+        const u32 *Ab = (const u32 *)(SR + (oA & ~3));
+        const int P0 = 32 * T * c.wave;
+        const v4i_t *Bb = (const v4i_t *)(TB + 32 * (P0 + r + 32) + 16 * h);   // block P0 + r (+32 pad)
+        v16i_t lo[T], hi[T];
+#pragma unroll
+        for (int f = 0; f < T; ++f) {
+            lo[f] = v16i_t{};
+            hi[f] = v16i_t{};
+        }
+        auto afrag = [&](int dd) {
+            const u32 *ap = Ab - 8 * dd;
+            const u32 w0 = ap[0], w1 = ap[1], w2 = ap[2], w3 = ap[3], w4 = ap[4];
+            v4i_t a;
+            a.x = (int)__builtin_amdgcn_alignbyte(w1, w0, sh);
+            a.y = (int)__builtin_amdgcn_alignbyte(w2, w1, sh);
+            a.z = (int)__builtin_amdgcn_alignbyte(w3, w2, sh);
+            a.w = (int)__builtin_amdgcn_alignbyte(w4, w3, sh);
+            return a;
+        };
+        constexpr int NM = T + D - 1;   // m = f - jj in [-(D-1), T-1] -> index m + D - 1
+        for (int k = 0; k < (ablate ? 0 : 32); ++k) {   // ablate: timing experiments only
+            for (int j0 = 0; k + 32 * j0 <= NB; j0 += D) {
+                v4i_t A[D];
+#pragma unroll
+                for (int jj = 0; jj < D; ++jj)
+                    if (k + 32 * (j0 + jj) <= NB) A[jj] = afrag(k + 32 * (j0 + jj));
+                v4i_t BL[NM], BH[NM];
+#pragma unroll
+                for (int mi = 0; mi < NM; ++mi) {
+                    const int m = mi - (D - 1);
+                    const int dm = k + 32 * (j0 - m);   // dd of the pair (f, jj) with f - jj = m
+                    // some (f, jj) with f - jj = m, f < T, jj < D, dd <= NB
+                    const int jlo = m < 0 ? -m : 0, jhi = (T - 1 - m) < (D - 1) ? (T - 1 - m) : (D - 1);
+                    const bool any = jlo <= jhi && k + 32 * (j0 + jlo) <= NB;
+                    const int boff = 32 * (m - j0) - k;   // in blocks, relative to Bb
+                    if (any && dm <= P0 + 31) BL[mi] = Bb[2 * boff];
+                    if (any && dm >= P0 + 1) BH[mi] = Bb[2 * boff + 2 * NB];
+                }
+#pragma unroll
+                for (int f = 0; f < T; ++f)
+#pragma unroll
+                    for (int jj = 0; jj < D; ++jj) {
+                        const int dd = k + 32 * (j0 + jj);
+                        const int mi = f - jj + D - 1;
+                        const int p0 = P0 + 32 * f;
+                        if (dd <= NB) {
+                            if (dd <= p0 + 31) lo[f] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[jj], BL[mi], lo[f], 0, 0, 0);
+                            if (dd >= p0 + 1) hi[f] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[jj], BH[mi], hi[f], 0, 0, 0);
+                        }
+                    }
+            }
+        }
+        i64 F[T][4];
+        const i64 PZt = PZ[L32];
+#pragma unroll
+        for (int f = 0; f < T; ++f) {
+            const int p0 = P0 + 32 * f;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int q = 8 * (p0 + r) + 2 * g + h;
+                const u32 u4 = __builtin_bswap32(*(const u32 *)(SR + 28 + L8 - 4 * q)) ^ 0x80808080u;
+                const u32 v4 = *(const u32 *)(TB + 1024 + 4 * q) ^ 0x80808080u;
+                i64 run = PZ[q], cz = 0, acc = 0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    run += (i64)((u4 >> (8 * e)) & 255) + (i64)((v4 >> (8 * e)) & 255) - 128;
+                    cz += run << (8 * e);
+                    acc += ((i64)lo[f][4 * g + e] - (i64)hi[f][4 * g + e]) << (8 * e);
+                }
+                F[f][g] = acc + 128 * (2 * cz - PZt * (i64)0x01010101);
+            }
+        }
+        __syncthreads();
+        i64 *DG = (i64 *)smem;
+#pragma unroll
+        for (int f = 0; f < T; ++f) {
+            const int p0 = P0 + 32 * f;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) DG[8 * (p0 + r) + 2 * g + h] = F[f][g];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int m = u * c.nt + c.t;
+            d[0][2 * u] = DG[2 * m];
+            d[0][2 * u + 1] = DG[2 * m + 1];
+        }
+    }
+    long slots[1] = {slot};
+    bool keep[1] = {true};
+    normalize_store<U, 1>(c, d, slots, keep, false, st, l, sm);
+}

@@ -182,12 +182,13 @@ static pass_fn get_pass(int U, int logg, int dir)
     return nullptr;
 }
 
-// pointwise kernel choice: 0 = int8 MFMA (k_pwm, l % 128 == 0), 1 = VALU MAC (k_pw).
-// MPFFT_POINTWISE=valu forces the VALU kernel (A/B parity and timing).
+// pointwise kernel choice: 0 = int8 MFMA register-blocked (k_pwm2, l % 256 == 0) else
+// k_pwm (l % 128 == 0), 1 = VALU MAC (k_pw), 2 = k_pwm even when k_pwm2 applies.
+// MPFFT_POINTWISE=valu / mfma1 force them (A/B parity and timing).
 static int pw_kind()
 {
     const char *e = getenv("MPFFT_POINTWISE");
-    return (e && !strcmp(e, "valu")) ? 1 : 0;
+    return (e && !strcmp(e, "valu")) ? 1 : (e && !strcmp(e, "mfma1")) ? 2 : 0;
 }
 
 // dynamic LDS above 64 KiB must be opted into per kernel (gfx950 has 160 KiB per CU)
@@ -383,7 +384,21 @@ struct Exec {
     {
         const long cnt = (long)rcount * P.NC;
         if (cnt == 0) return MPFFT_OK;
-        if (P.l % 128 == 0 && pw_kind() == 0) {   // int8 MFMA Toeplitz product
+        static const long pwm2_maxl = [] { const char *e = getenv("MPFFT_PWM2_MAXL"); return e ? atol(e) : 4096L; }();
+        if (P.l % 256 == 0 && P.l <= pwm2_maxl && pw_kind() == 0) {   // int8 MFMA, register-blocked: 2 fold tiles per wave
+            const int nw = (int)P.l / 256;
+            const int tpb = 64 * nw;
+            const size_t lds = pwm_lds_bytes((int)P.l, 4, nw);
+            void (*f)(u64 *, u64 *, int *, const u64 *, const int *, int, int) =
+                getenv("MPFFT_PWM2_D4") && nw <= 8 ? k_pwm2<4, 2, 4> : k_pwm2<4, 2, 2>;   // D = 4: more VGPRs, slower at C2
+            const char *ea = getenv("MPFFT_PWABLATE");   // timing experiments only: 1 = no MFMA phase
+            allow_lds((const void *)f, lds);
+            hipLaunchKernelGGL(f, dim3((unsigned)cnt), dim3(tpb), lds, s, row.dig[0], row.cb[0], row.top[0],
+                               (const u64 *)row.dig[1], (const int *)row.top[1], (int)P.l, ea ? atoi(ea) : 0);
+            HIPCHK(hipGetLastError());
+            return MPFFT_OK;
+        }
+        if (P.l % 128 == 0 && pw_kind() != 1) {   // int8 MFMA Toeplitz product
             const int nw = std::min((int)P.l / 128, 16);
             const int tpb = 64 * nw;
             const int U = (int)P.l / tpb;
@@ -618,6 +633,33 @@ struct Exec {
 
     int combine_single(u64 *r, unsigned char *ws)
     {
+        static const bool multi = [] { const char *e = getenv("MPFFT_COMBINE"); return e && !strcmp(e, "multi"); }();
+        if (!multi) {   // one launch: window sums + decoupled look-back carries (k_combine1)
+            CombArgs a;
+            a.dig = row.dig[0];
+            a.l = (int)P.l;
+            a.N = P.N;
+            a.bits1 = P.bits1;
+            a.len = P.len;
+            a.m0 = 0;
+            a.mcount = P.total;
+            a.kbase = 0;
+            a.halo = nullptr;
+            a.H = 0;
+            a.NC = (int)P.NC;
+            a.cbb = cbb;
+            a.ccb = ccb;
+            a.cbs = cbs;
+            a.r0 = r0;
+            a.lo64 = nullptr;
+            a.hi32 = nullptr;
+            const long nb = (P.total + CB_LIMBS - 1) / CB_LIMBS;
+            u32 *st = (u32 *)(ws + P.off_lo);   // (nb + 1) flags, inside the lo64 scratch of the multi-kernel path
+            HIPCHK(hipMemsetAsync(st, 0, (size_t)(nb + 4) / 4 * 16, s));   // whole 16-byte words: one fill
+            hipLaunchKernelGGL(k_combine1, dim3((unsigned)nb), dim3(256), 0, s, a, r, st);
+            HIPCHK(hipGetLastError());
+            return MPFFT_OK;
+        }
         return combine(r, 0, P.total, 0, nullptr, 0, (u64 *)(ws + P.off_lo), (u32 *)(ws + P.off_hi),
                        ws + P.off_bg, ws + P.off_bp, ws + P.off_bc, 0, nullptr, false);
     }

@@ -30,7 +30,7 @@ def torch_dev():
 STAGE_SHAPES = [(6, 1, 3, 2), (6, 1, 1, 1), (7, 1, 5, 4), (7, 3, 13, 2), (8, 2, 30, 25), (8, 4, 60, 50),
                 (9, 1, 30, 31), (10, 3, 300, 200), (11, 1, 1000, 1000), (5, 2, 2, 1), (4, 4, 1, 1),
                 (3, 8, 1, 1), (2, 16, 1, 1)]
-# coefficient sizes l = 128 ... 4096 limbs: the int8-MFMA pointwise (k_pwm<2,1>, k_pwm<4,2>)
+# coefficient sizes l = 128 ... 4096 limbs: the int8-MFMA pointwise (k_pwm, k_pwm2)
 MFMA_SHAPES = [(9, 16, 2000, 1500), (8, 64, 3000, 2000), (7, 256, 4000, 3000), (6, 1024, 6000, 5000),
                (5, 4096, 8000, 8000), (6, 4096, 20000, 20000)]
 
@@ -109,12 +109,13 @@ def _pattern(kind, l, N, rng):
     return v, 0
 
 
-@pytest.mark.parametrize("kind", ["mfma", "valu"])
-@pytest.mark.parametrize("depth,w", [(11, 1), (9, 16), (8, 64), (7, 256), (6, 1024), (6, 4096)])
+@pytest.mark.parametrize("kind", ["mfma", "mfma1", "valu"])
+@pytest.mark.parametrize("depth,w", [(11, 1), (9, 16), (8, 64), (7, 256), (6, 1024), (5, 4096), (6, 4096)])
 def test_pointwise_direct(mp, torch_dev, kind, depth, w):
     """The pointwise stage alone on hand-placed canonical inputs (every pair of the
     special values 0, 1, 2^N - 1, 2^N, 0x80.. and 0x7f.. bytes, random), for the
-    int8-MFMA kernel (l % 128 == 0) and the VALU kernel (MPFFT_POINTWISE=valu)."""
+    int8-MFMA kernels (k_pwm2 when l % 256 == 0, k_pwm when l % 128 == 0 or
+    MPFFT_POINTWISE=mfma1) and the VALU kernel (MPFFT_POINTWISE=valu)."""
     import torch
     from gpu_stages import _cbs, _val_reduced
     mx = max_limbs(depth, w)
