@@ -49,7 +49,21 @@ struct PassArgs {
     int nbuf;            // LDS staging buffers (1 or 2)
     u64 scale_e;         // wave kernels: nonzero = fused final scaling by 2^scale_e (canonical store)
     int ablate;          // timing experiments only (MPFFT_ABLATE): 1 = no levels/twiddles, 2 = also no normalisation
+    unsigned *zp;        // non-null: clear zp[0, zn) (the combine's look-back flags) -- saves a fill launch
+    long zn;
 };
+
+// Grid-stride clear of PassArgs::zp; called at the top of every pass kernel, before
+// any barrier, so it cannot change the kernel's synchronisation.
+__device__ inline void pass_clear_flags(const PassArgs &a)
+{
+    if (!a.zp) return;
+    const long nt = (long)blockDim.x * blockDim.y * blockDim.z;
+    const long nthr = (long)gridDim.x * gridDim.y * gridDim.z * nt;
+    const long bid = ((long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    const long t = bid * nt + ((long)threadIdx.z * blockDim.y + threadIdx.y) * blockDim.x + threadIdx.x;
+    for (long i = t; i < a.zn; i += nthr) a.zp[i] = 0u;
+}
 
 // LDS carve for the coefficient kernels:
 //   [stage: rb * 2l i64][edge: norm_edge_ints int32][scan scratch: norm_scr_u64 u64]
@@ -144,6 +158,7 @@ __device__ __forceinline__ void normalize_store(const WG &c, const i64 (&x)[G][2
 template <int U, int LOGG, int DIR>
 __global__ __launch_bounds__(MPF_LB(U)) void k_pass(PassArgs a)
 {
+    pass_clear_flags(a);
     constexpr int G = 1 << LOGG;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const WG c = wg_ctx();

@@ -102,6 +102,7 @@ __device__ __forceinline__ void lp_levels(i64 *lds, const PassArgs &a, int pos0,
 template <int U, bool F, int LOGG, int DIR>
 __global__ __launch_bounds__(32 << LOGG) void k_lpass(PassArgs a)
 {
+    pass_clear_flags(a);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     i64 *lds = (i64 *)smem;
     const int lane = wv_lane();

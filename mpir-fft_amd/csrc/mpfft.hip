@@ -218,8 +218,14 @@ struct Exec {
     View col, row;
     int c0, ccount, r0, rcount, ccb, cbb;
     long cbs;
+    u32 *zflags = nullptr;   // non-null: the first forward column pass clears the combine's look-back flags
+    long zflags_n = 0;       // (u32 words), so combine_single needs no separate fill launch
 
     Exec(const Plan &p, hipStream_t st) : P(p), s(st) { nw = P.tpb / 64; }
+
+    long comb_blocks() const { return (P.total + CB_LIMBS - 1) / CB_LIMBS; }
+    u32 *comb_flags(unsigned char *ws) const { return (u32 *)(ws + P.off_lo); }
+    long comb_flag_words() const { return (comb_blocks() + 4) / 4 * 4; }
 
     // single-GPU workspace: both layouts are the natural one
     void single(unsigned char *ws)
@@ -349,6 +355,8 @@ struct Exec {
                 a.src[0] = srcA; a.nsrc[0] = nA;
                 a.src[1] = srcB; a.nsrc[1] = nB;
                 a.zero_from = (int)P.Tr;
+                a.zp = zflags;
+                a.zn = zflags_n;
             } else {
                 a.zero_from = (int)P.NR;
             }
@@ -653,9 +661,10 @@ struct Exec {
             a.r0 = r0;
             a.lo64 = nullptr;
             a.hi32 = nullptr;
-            const long nb = (P.total + CB_LIMBS - 1) / CB_LIMBS;
-            u32 *st = (u32 *)(ws + P.off_lo);   // (nb + 1) flags, inside the lo64 scratch of the multi-kernel path
-            HIPCHK(hipMemsetAsync(st, 0, (size_t)(nb + 4) / 4 * 16, s));   // whole 16-byte words: one fill
+            const long nb = comb_blocks();
+            u32 *st = comb_flags(ws);   // (nb + 1) flags, inside the lo64 scratch of the multi-kernel path
+            if (zflags != st)           // not already cleared by the first forward column pass
+                HIPCHK(hipMemsetAsync(st, 0, (size_t)comb_flag_words() * 4, s));   // whole 16-byte words: one fill
             hipLaunchKernelGGL(k_combine1, dim3((unsigned)nb), dim3(256), 0, s, a, r, st);
             HIPCHK(hipGetLastError());
             return MPFFT_OK;
@@ -669,6 +678,8 @@ static int run_all(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, un
 {
     Exec X(P, s);
     X.single(ws);
+    X.zflags = X.comb_flags(ws);
+    X.zflags_n = X.comb_flag_words();
     int rc;
     if ((rc = X.fwd_columns(d_i1, P.n1, d_i2, P.n2, 2))) return rc;
     if ((rc = X.fwd_rows(2))) return rc;

@@ -74,6 +74,7 @@ __device__ __forceinline__ void wv_levels(i64 (&x)[1 << LOGG][2 * U], const Pass
 template <int U, bool F, int LOGG, int DIR>
 __global__ __launch_bounds__(64 * WPB) void k_wpass(PassArgs a)
 {
+    pass_clear_flags(a);
     constexpr int G = 1 << LOGG;
     constexpr int NS = wv_stage_slots(G, U);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
