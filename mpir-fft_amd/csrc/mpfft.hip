@@ -223,6 +223,14 @@ struct Exec {
 
     Exec(const Plan &p, hipStream_t st) : P(p), s(st) { nw = P.tpb / 64; }
 
+    // levels in the next pass when `rem` remain: the fewest passes of <= maxlogg
+    // levels, balanced (C1 column inverse: 4 + 3 beats 5 + 2 by ~5 us)
+    int split(int rem) const
+    {
+        const int np = (rem + P.maxlogg - 1) / P.maxlogg;
+        return (rem + np - 1) / np;
+    }
+
     long comb_blocks() const { return (P.total + CB_LIMBS - 1) / CB_LIMBS; }
     u32 *comb_flags(unsigned char *ws) const { return (u32 *)(ws + P.off_lo); }
     long comb_flag_words() const { return (comb_blocks() + 4) / 4 * 4; }
@@ -349,7 +357,7 @@ struct Exec {
     {
         int lvl = 0;
         while (lvl < P.lbR) {
-            int k = P.lbR - lvl < P.maxlogg ? P.lbR - lvl : P.maxlogg;
+            int k = split(P.lbR - lvl);
             PassArgs a = col_args();
             if (lvl == 0) {
                 a.src[0] = srcA; a.nsrc[0] = nA;
@@ -376,7 +384,7 @@ struct Exec {
     {
         int lvl = 0;
         while (lvl < P.lbC) {
-            int k = P.lbC - lvl < P.maxlogg ? P.lbC - lvl : P.maxlogg;
+            int k = split(P.lbC - lvl);
             PassArgs a = row_args();
             a.lvl0 = lvl;
             a.tw_mode = lvl == 0 ? 1 : 0;
@@ -452,7 +460,7 @@ struct Exec {
     {
         int hi = P.lbC;
         while (hi > 0) {
-            int k = hi < P.maxlogg ? hi : P.maxlogg;
+            int k = split(hi);
             PassArgs a = row_args();
             a.lvl0 = hi - k;
             a.tw_mode = (hi - k == 0) ? 2 : 0;
@@ -469,7 +477,7 @@ struct Exec {
         const int lbM = ilog2(m);
         int hi = lbM;
         while (hi > 0) {
-            int k = hi < P.maxlogg ? hi : P.maxlogg;
+            int k = split(hi);
             PassArgs a = col_args();
             a.lbM = lbM;
             a.lvl0 = hi - k;
