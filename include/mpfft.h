@@ -47,9 +47,14 @@ extern "C" {
 void new_mpn_mul(mp_limb_t *r1, mp_limb_t *i1, mp_size_t n1, mp_limb_t *i2, mp_size_t n2,
                  mp_bitcnt_t depth, mp_bitcnt_t w);
 
-/* Same as new_mpn_mul, returning MPFFT_* instead of aborting. */
+/* Same as new_mpn_mul, returning MPFFT_* instead of aborting.  Host pointers.
+ * Thread-safe: the calling thread's current HIP device (hipSetDevice) selects a
+ * per-device context (stream + grow-only workspace); calls on one device serialise. */
 int mpfft_mul_ex(uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i2, long n2,
                  unsigned long depth, unsigned long w);
+
+/* Free the calling thread's device context buffers (re-allocated by the next call). */
+int mpfft_release(void);
 
 /* Device-resident multiply: all pointers are device memory, work is queued on
  * `stream` (a hipStream_t, NULL = default) and not synchronised.  d_ws must hold

@@ -65,6 +65,8 @@ def lib():
         h.new_mpn_mul.restype = None
         h.mpfft_mul_ex.argtypes = [_u64p, _u64p, _L, _u64p, _L, _UL, _UL]
         h.mpfft_mul_ex.restype = ctypes.c_int
+        h.mpfft_release.argtypes = []
+        h.mpfft_release.restype = ctypes.c_int
         h.mpfft_mul_device.argtypes = [_vp, _vp, _L, _vp, _L, _UL, _UL, _vp, ctypes.c_size_t, _vp]
         h.mpfft_mul_device.restype = ctypes.c_int
         h.mpfft_stage.argtypes = [ctypes.c_int, _vp, _vp, _vp, _L, _L, _UL, _UL, _vp, ctypes.c_size_t, _vp]

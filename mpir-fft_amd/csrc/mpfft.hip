@@ -862,13 +862,31 @@ int mpfft_shard_combine(const mpfft_shard *sh, int phase, uint64_t *d_r, long m0
     return X.combine(d_r, m0, mcount, kbase, halo, H, lo, hi, bg, bp, bc, cin, d_sum, phase == 1);
 }
 
-// host-pointer entry with status
-static std::mutex g_mu;
-static unsigned char *g_ws = nullptr;
-static size_t g_ws_bytes = 0;
-static u64 *g_io = nullptr;
-static size_t g_io_bytes = 0;
-static hipStream_t g_stream = nullptr;
+// host-pointer entry with status.  One context per device (SURVEY 8b "Threading"):
+// the calling thread's current HIP device selects it, so threads driving different
+// GPUs never share memory or streams; threads on the same device serialise on its lock.
+struct DevCtx {
+    std::mutex mu;
+    unsigned char *ws = nullptr;
+    size_t ws_bytes = 0;
+    u64 *io = nullptr;
+    size_t io_bytes = 0;
+    hipStream_t stream = nullptr;
+};
+static const int MPFFT_MAX_DEV = 64;
+static DevCtx g_dev[MPFFT_MAX_DEV];
+
+// grow-only device buffer owned by a DevCtx
+static int ensure_buf(void **p, size_t *have, size_t need)
+{
+    if (*have >= need) return MPFFT_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *have = 0;
+    if (hipMalloc(p, need) != hipSuccess) return MPFFT_ENOMEM;
+    *have = need;
+    return MPFFT_OK;
+}
 
 int mpfft_mul_ex(uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i2, long n2, unsigned long depth,
                  unsigned long w)
@@ -876,33 +894,37 @@ int mpfft_mul_ex(uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i2, 
     Plan P;
     int rc = make_plan(&P, n1, n2, depth, w);
     if (rc) return rc;
-    std::lock_guard<std::mutex> lk(g_mu);
     (void)hipGetLastError();
-    int ndev = 0;
+    int ndev = 0, dev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return MPFFT_ENODEV;
-    if (!g_stream) HIPCHK(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
-    if (g_ws_bytes < P.bytes) {
-        if (g_ws) (void)hipFree(g_ws);
-        g_ws = nullptr;
-        g_ws_bytes = 0;
-        if (hipMalloc((void **)&g_ws, P.bytes) != hipSuccess) return MPFFT_ENOMEM;
-        g_ws_bytes = P.bytes;
-    }
-    const size_t io = (size_t)2 * (n1 + n2) * 8;
-    if (g_io_bytes < io) {
-        if (g_io) (void)hipFree(g_io);
-        g_io = nullptr;
-        g_io_bytes = 0;
-        if (hipMalloc((void **)&g_io, io) != hipSuccess) return MPFFT_ENOMEM;
-        g_io_bytes = io;
-    }
-    u64 *d_i1 = g_io, *d_i2 = g_io + n1, *d_r = g_io + n1 + n2;
-    HIPCHK(hipMemcpyAsync(d_i1, i1, (size_t)n1 * 8, hipMemcpyHostToDevice, g_stream));
-    HIPCHK(hipMemcpyAsync(d_i2, i2, (size_t)n2 * 8, hipMemcpyHostToDevice, g_stream));
-    rc = run_all(P, d_r, d_i1, d_i2, g_ws, g_stream);
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MPFFT_MAX_DEV) return MPFFT_ENODEV;
+    DevCtx &C = g_dev[dev];
+    std::lock_guard<std::mutex> lk(C.mu);
+    if (!C.stream) HIPCHK(hipStreamCreateWithFlags(&C.stream, hipStreamNonBlocking));
+    if ((rc = ensure_buf((void **)&C.ws, &C.ws_bytes, P.bytes))) return rc;
+    if ((rc = ensure_buf((void **)&C.io, &C.io_bytes, (size_t)2 * (n1 + n2) * 8))) return rc;
+    u64 *d_i1 = C.io, *d_i2 = C.io + n1, *d_r = C.io + n1 + n2;
+    HIPCHK(hipMemcpyAsync(d_i1, i1, (size_t)n1 * 8, hipMemcpyHostToDevice, C.stream));
+    HIPCHK(hipMemcpyAsync(d_i2, i2, (size_t)n2 * 8, hipMemcpyHostToDevice, C.stream));
+    rc = run_all(P, d_r, d_i1, d_i2, C.ws, C.stream);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(r1, d_r, (size_t)(n1 + n2) * 8, hipMemcpyDeviceToHost, g_stream));
-    HIPCHK(hipStreamSynchronize(g_stream));
+    HIPCHK(hipMemcpyAsync(r1, d_r, (size_t)(n1 + n2) * 8, hipMemcpyDeviceToHost, C.stream));
+    HIPCHK(hipStreamSynchronize(C.stream));
+    return MPFFT_OK;
+}
+
+// release the calling device's cached workspace (the next call re-allocates)
+int mpfft_release(void)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MPFFT_MAX_DEV) return MPFFT_ENODEV;
+    DevCtx &C = g_dev[dev];
+    std::lock_guard<std::mutex> lk(C.mu);
+    if (C.ws) (void)hipFree(C.ws);
+    if (C.io) (void)hipFree(C.io);
+    C.ws = nullptr;
+    C.io = nullptr;
+    C.ws_bytes = C.io_bytes = 0;
     return MPFFT_OK;
 }
 

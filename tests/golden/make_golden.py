@@ -5,7 +5,9 @@ from (n, seed) with the splitmix64/xoshiro256** stream shared by the product
 Expected outputs are the exact products: Python int multiplication for the
 small and C0/C1 shapes (independent of GMP), GMP mpn_mul -- the reference's own
 integration-test oracle (mul_fft.c:5542) -- for the 10^9-bit configs.
-Run: python tests/golden/make_golden.py [--big]
+Run: python tests/golden/make_golden.py [--big]        (everything; --big adds C2-C4)
+     python tests/golden/make_golden.py --add C4       (compute only the named entries and
+                                                       merge them into products.json)
 """
 import hashlib
 import json
@@ -34,6 +36,8 @@ BIG = [
 HUGE = [
     ("C2", 15, 4, 15625000, 15625000, 0x1001, 0x2002),
     ("C3", 15, 4, 20312500, 20312500, 0x1001, 0x2002),
+    # BASELINE configs[4]: the 10^10-bit north-star multiply (GMP mpn_mul: ~3 min, 5 GB of RAM)
+    ("C4", 17, 2, 156250000, 156250000, 0x1001, 0x2002),
 ]
 
 
@@ -43,10 +47,17 @@ def as_int(a):
 
 def main():
     out = []
-    for name, depth, w, n1, n2, s1, s2 in SMALL + BIG + (HUGE if "--big" in sys.argv else []):
+    todo = SMALL + BIG + (HUGE if "--big" in sys.argv else [])
+    path = os.path.join(HERE, "products.json")
+    if "--add" in sys.argv:
+        names = set(sys.argv[sys.argv.index("--add") + 1].split(","))
+        todo = [c for c in SMALL + BIG + HUGE if c[0] in names]
+        with open(path) as f:
+            out = [c for c in json.load(f) if c["name"] not in names]
+    for name, depth, w, n1, n2, s1, s2 in todo:
         a = O.fill_random(n1, s1)
         b = O.fill_random(n2, s2)
-        if name in ("C2", "C3"):
+        if name in ("C2", "C3", "C4"):
             r = O.gmp_mul(a, b)
             src = "gmp mpn_mul"
         else:
@@ -59,7 +70,9 @@ def main():
             c["product_hex"] = format(as_int(r), "x")
         out.append(c)
         print(name, c["sha256"][:16], src, flush=True)
-    with open(os.path.join(HERE, "products.json"), "w") as f:
+    order = [c[0] for c in SMALL + BIG + HUGE]
+    out.sort(key=lambda c: order.index(c["name"]))
+    with open(path, "w") as f:
         json.dump(out, f, indent=1)
 
 
