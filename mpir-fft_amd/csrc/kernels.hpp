@@ -51,6 +51,7 @@ struct PassArgs {
     int ablate;          // timing experiments only (MPFFT_ABLATE): 1 = no levels/twiddles, 2 = also no normalisation
     unsigned *zp;        // non-null: clear zp[0, zn) (the combine's look-back flags) -- saves a fill launch
     long zn;
+    unsigned long long *dbg;   // diagnostics only (MPFFT_BP_STAMPS): per-workgroup s_memtime phase stamps
 };
 
 // Grid-stride clear of PassArgs::zp; called at the top of every pass kernel, before

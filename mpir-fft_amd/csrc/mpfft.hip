@@ -29,6 +29,8 @@
 #include "kernels.hpp"
 #include "combine.hpp"
 #include "wdispatch.hpp"
+#include "bdispatch.hpp"
+#include "pdispatch.hpp"
 #include "../../include/mpfft.h"
 
 // ---------------------------------------------------------------------------
@@ -60,6 +62,7 @@ struct Plan {
     bool wfull;         // l == 64 wU
     bool fuse_scale;    // scaling fused into the last inverse column pass (no truncation)
     bool lds;           // LDS-resident radix-2^5 passes (lkernels.hpp)
+    bool big;           // LDS-resident passes for 512 <= l <= 4096 (bkernels.hpp)
     size_t slots;       // allocated slots per operand
     size_t off_digA, off_topA, off_cbA, off_digB, off_topB, off_cbB, off_lo, off_hi, off_bg, off_bp, off_bc, bytes;
     long nblk;
@@ -122,6 +125,18 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
             p->maxlogg = LP_MAXLOGG;
             if (e && atoi(e) >= 1 && atoi(e) <= LP_MAXLOGG) p->maxlogg = atoi(e);
         }
+    }
+    {
+        const char *e = getenv("MPFFT_BIG");
+        const long rows = p->l / 64;
+        p->big = !p->wave && p->l >= 512 && p->l % 64 == 0 && !(rows & (rows - 1)) && !(e && !strcmp(e, "0"));
+    }
+    if (p->big) {   // as many levels per pass as coefficients fit in LDS (G <= 16)
+        int lg = 1;
+        while (lg < BP_MAXLOGG && bp_lds_need(p->l, 2 << lg) <= BP_LDS_MAX) ++lg;
+        p->maxlogg = lg;
+        const char *e = getenv("MPFFT_BLOGG");
+        if (e && atoi(e) >= 1 && atoi(e) <= lg) p->maxlogg = atoi(e);
     }
     p->slots = (size_t)2 * p->n;
     size_t o = 0;
@@ -264,6 +279,22 @@ struct Exec {
 
     int pass(PassArgs a, int logg, int dir, int nops)
     {
+        if (P.big) {
+            // limb-aligned kernel unless some rotation of the pass has a sub-limb part
+            const bool gen = (a.rho % 64) || (a.tw_mode && a.tw_w % 64) || (a.scale_e % 64);
+            bp_fn f = gen ? bp_get_gen(logg, dir) : bp_get(logg, dir);
+            if (!f) return MPFFT_EUNSUPPORTED;
+            const size_t lds = bp_lds_need((int)P.l, 1 << logg);
+            allow_lds((const void *)f, lds);
+            a.ngroups = 1 << (a.lbM - logg);
+            dim3 grid((unsigned)((long)a.nsub * a.ngroups), (unsigned)nops);
+            const unsigned nthr = (unsigned)(64 * bp_waves((int)P.l, logg));
+            static const bool stamps = getenv("MPFFT_BP_STAMPS") != nullptr;
+            if (stamps) return bp_stamped(f, grid, nthr, lds, a, logg, dir);
+            hipLaunchKernelGGL(f, grid, dim3(nthr), lds, s, a);
+            HIPCHK(hipGetLastError());
+            return MPFFT_OK;
+        }
         if (P.wave && P.lds) {
             pass_fn f = wv_fns(P.wU, P.wfull).lpass(logg, dir);
             if (!f) return MPFFT_EUNSUPPORTED;
@@ -302,6 +333,41 @@ struct Exec {
         dim3 grid((unsigned)((long)a.nsub * a.ngroups), (unsigned)nops);
         hipLaunchKernelGGL(f, grid, dim3(P.tpb), lds_pass, s, a);
         HIPCHK(hipGetLastError());
+        return MPFFT_OK;
+    }
+
+    // diagnostics only (MPFFT_BP_STAMPS): run one k_bpass launch with per-workgroup phase
+    // stamps and print the average phase lengths (s_memtime ticks) of the working groups
+    int bp_stamped(bp_fn f, dim3 grid, unsigned nthr, size_t lds, PassArgs a, int logg, int dir)
+    {
+        const size_t nwg = (size_t)grid.x * grid.y;
+        unsigned long long *d = nullptr;
+        HIPCHK(hipMalloc((void **)&d, nwg * 64));
+        HIPCHK(hipMemsetAsync(d, 0, nwg * 64, s));
+        a.dbg = d;
+        hipLaunchKernelGGL(f, grid, dim3(nthr), lds, s, a);
+        HIPCHK(hipGetLastError());
+        unsigned long long *h = (unsigned long long *)malloc(nwg * 64);
+        HIPCHK(hipMemcpyAsync(h, d, nwg * 64, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        double sum[8] = {0};
+        long cnt = 0;
+        unsigned long long t0 = ~0ull, t1 = 0;
+        for (size_t w = 0; w < nwg; ++w) {
+            const unsigned long long *q = h + 8 * w;
+            if (!q[7]) continue;   // skipped group (past the truncation point)
+            ++cnt;
+            if (q[0] < t0) t0 = q[0];
+            if (q[7] > t1) t1 = q[7];
+            unsigned long long prev = q[0];
+            for (int k = 1; k < 8; ++k)
+                if (q[k]) { sum[k] += (double)(q[k] - prev); prev = q[k]; }
+        }
+        fprintf(stderr, "bp_stamps logg=%d dir=%d l=%ld groups=%ld/%zu span=%llu ticks: load %.0f lv0 %.0f lv1 %.0f lv2 %.0f lv3 %.0f canon %.0f store %.0f\n",
+                logg, dir, P.l, cnt, nwg, t1 - t0, sum[1] / cnt, sum[2] / cnt, sum[3] / cnt, sum[4] / cnt, sum[5] / cnt,
+                sum[6] / cnt, sum[7] / cnt);
+        free(h);
+        (void)hipFree(d);
         return MPFFT_OK;
     }
 
@@ -396,10 +462,35 @@ struct Exec {
         return MPFFT_OK;
     }
 
+    // nested negacyclic pointwise (pkernels.hpp) for big coefficients: (l -> pieces 2^lk)
+    static int pwss_lk(long l)
+    {
+        const char *e = getenv("MPFFT_PWSS");
+        if (e && !strcmp(e, "0")) return 0;
+        switch (l) {
+        case 1024: return getenv("MPFFT_PWSS1024") ? 8 : 0;   // MFMA schoolbook still wins below 2048 (to measure)
+        case 2048: return 8;
+        case 4096: return 9;
+        }
+        return 0;
+    }
+
     int pointwise()
     {
         const long cnt = (long)rcount * P.NC;
         if (cnt == 0) return MPFFT_OK;
+        if (const int lk = pwss_lk(P.l)) {
+            const int M = pw_inner_limbs(P.l, lk);
+            pw_fn f = pw_get(M);
+            if (f) {
+                const size_t lds = pw_lds(M, 1 << lk, (int)P.l);
+                allow_lds((const void *)f, lds);
+                hipLaunchKernelGGL(f, dim3((unsigned)cnt), dim3(1u << lk), lds, s, row.dig[0], row.cb[0], row.top[0],
+                                   (const u64 *)row.dig[1], (const int *)row.top[1], (int)P.l, lk);
+                HIPCHK(hipGetLastError());
+                return MPFFT_OK;
+            }
+        }
         static const long pwm2_maxl = [] { const char *e = getenv("MPFFT_PWM2_MAXL"); return e ? atol(e) : 4096L; }();
         if (P.l % 256 == 0 && P.l <= pwm2_maxl && pw_kind() == 0) {   // int8 MFMA, register-blocked: 2 fold tiles per wave
             const int nw = (int)P.l / 256;

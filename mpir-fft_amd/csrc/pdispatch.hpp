@@ -1,0 +1,21 @@
+// pdispatch.hpp -- host-side view of the nested negacyclic pointwise kernel (pkernels.hpp)
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+typedef void (*pw_fn)(uint64_t *, uint64_t *, int *, const uint64_t *, const int *, int, int);
+
+pw_fn pw_get(int M);               // k_pwss<M> (M = inner coefficient limbs), nullptr if not built
+size_t pw_lds(int M, int K, int l);
+
+// Inner ring for a product mod 2^(64 l) + 1 cut into K = 2^lk pieces: the smallest M
+// (limbs) with 64 M >= 2 (64 l / K) + lk + 2 and 64 M a multiple of K (theta = 2^(64 M / K)).
+inline int pw_inner_limbs(long l, int lk)
+{
+    const long K = 1L << lk, B = 64 * l / K;
+    const long need = 2 * B + lk + 2;
+    const long step = K / 64 > 1 ? K / 64 : 1;   // M multiple of K / 64
+    long M = (need + 63) / 64;
+    M = (M + step - 1) / step * step;
+    return (int)M;
+}
