@@ -9,7 +9,7 @@ typedef void (*bp_fn)(PassArgs);
 #define BP_WAVES 16           // at most (G l <= 16384 limbs)
 #define BP_RMAX 8             // rows of 64 limbs per wave per level: a wave owns 8 rows of one pair
 #define BP_SB 4               // rows per wave in flight in the store phase
-#define BP_LB 4               // 16-byte loads in flight per thread in the load phase
+#define BP_LB 8               // 16-byte loads in flight per thread in the load phase
 #define BP_LDS_MAX (160 * 1024)
 
 bp_fn bp_get(int logg, int dir);       // k_bpass<logg, dir, false>: every rotation limb-aligned

@@ -54,6 +54,18 @@ __device__ __forceinline__ BSlot bp_slot(unsigned char *lds, int s, int l)
 
 __device__ __forceinline__ i64 bp_cneg(i64 v, bool n) { return n ? -v : v; }
 
+// bit j of x -> bit 2j of the result (Morton spread)
+__device__ __forceinline__ u64 bp_spread(u32 x)
+{
+    u64 v = x;
+    v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+    v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+    v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    v = (v | (v << 2)) & 0x3333333333333333ull;
+    v = (v | (v << 1)) & 0x5555555555555555ull;
+    return v;
+}
+
 // low / high part of D * 2^b split at 32 bits (D a signed digit, 0 <= b < 32): D 2^b = hi 2^32 + lo
 __device__ __forceinline__ i64 bp_lo(i64 D, int b) { return (i64)(((u64)(u32)D << b) & MPF_M32); }
 __device__ __forceinline__ i64 bp_hi(i64 D, int b)
@@ -570,45 +582,55 @@ __global__ __launch_bounds__(64 * BP_WAVES) void k_bpass(PassArgs a)
         __syncthreads();
     }
     if (stamp && threadIdx.x == 0) stamp[6] = __builtin_amdgcn_s_memtime();
+    // 128-limb blocks, 2 limbs per lane: 16-byte stores (one 1 KB wave instruction per block)
     const int cbw = cb_words(l);
-    const int items = G * rows;   // (slot, row) pairs, wave t handles t, t + nwv, ...; batches of BP_SB
+    const int bpr = rows >> 1;                    // blocks per slot
+    const int items = G * bpr;                    // wave t handles t, t + nwv, ...; batches of BP_SB
+    typedef unsigned long long v2u __attribute__((ext_vector_type(2)));
     for (int t0 = wave; t0 < items; t0 += BP_SB * nwv) {
-        u64 f[BP_SB];
-        int c[BP_SB];
+        v2u f[BP_SB];
+        short c[BP_SB];
 #pragma unroll
         for (int q = 0; q < BP_SB; ++q) {
             const int t = t0 + q * nwv;
-            f[q] = 0;
+            f[q] = v2u{0, 0};
             c[q] = 0;
             if (t < items) {
-                const int i = t >> lrows, u = t & (rows - 1);
+                const int i = t >> (lrows - 1), v = t & (bpr - 1);
                 const BSlot b = bp_slot(smem, i, l);
-                f[q] = b.f[64 * u + lane];
-                c[q] = a.canon ? 0 : b.c[64 * u + lane];
+                const int m = 128 * v + 2 * lane;
+                f[q] = *(const v2u *)(b.f + m);
+                c[q] = a.canon ? 0 : *(const short *)(b.c + m);
             }
         }
 #pragma unroll
         for (int q = 0; q < BP_SB; ++q) {
             const int t = t0 + q * nwv;
             if (t >= items) continue;
-            const int i = t >> lrows, u = t & (rows - 1);
+            const int i = t >> (lrows - 1), v = t & (bpr - 1);
             const bool keep = DIR == 1 || ((g.pos0 + i * g.pstep) & ~(g.pstep - 1)) < a.need;
             if (!keep) continue;   // wave-uniform
             const long sl = wv_uniform(slot_of(i));
-            const int m = 64 * u + lane;
+            const int m = 128 * v + 2 * lane;
             u64 *dst = st.dig + (size_t)sl * l;
             u64 *cbp = st.cb + (size_t)sl * cbw;
             // f_m + c_m = nf + kout 2^64: limb + carry out of limb m (mask bit m; out of
             // limb l-1 it weighs 2^N == -1, as load_coeff reads it back).  Canonical: c == 0.
-            const u64 nf = f[q] + (u64)(i64)c[q];
-            const int kout = c[q] >= 0 ? (int)(nf < f[q]) : -(int)(nf > f[q]);
-            dst[m] = nf;
-            const u64 pm = __ballot(kout == 1), nm = __ballot(kout == -1);
-            if (lane == 0) {
-                typedef unsigned long long v2u __attribute__((ext_vector_type(2)));
-                *(v2u *)(cbp + 2 * u) = v2u{pm, nm};
+            const int c0 = (signed char)(c[q] & 0xff), c1 = (signed char)((unsigned short)c[q] >> 8);
+            const u64 n0 = f[q].x + (u64)(i64)c0, n1 = f[q].y + (u64)(i64)c1;
+            const int k0 = c0 >= 0 ? (int)(n0 < f[q].x) : -(int)(n0 > f[q].x);
+            const int k1 = c1 >= 0 ? (int)(n1 < f[q].y) : -(int)(n1 > f[q].y);
+            *(v2u *)(dst + m) = v2u{n0, n1};
+            // mask words of rows 2v (lanes 0..31) and 2v+1: even/odd limb ballots, bit-interleaved
+            const u64 pe = __ballot(k0 == 1), po = __ballot(k1 == 1);
+            const u64 ne = __ballot(k0 == -1), no = __ballot(k1 == -1);
+            if (lane < 2) {
+                const int sh = 32 * lane;
+                const u64 pw = bp_spread((u32)(pe >> sh)) | (bp_spread((u32)(po >> sh)) << 1);
+                const u64 nw = bp_spread((u32)(ne >> sh)) | (bp_spread((u32)(no >> sh)) << 1);
+                *(v2u *)(cbp + 4 * v + 2 * lane) = v2u{pw, nw};
             }
-            if (u == 0 && lane == 0) st.top[sl] = a.canon ? ctop[i] : 0;
+            if (v == 0 && lane == 0) st.top[sl] = a.canon ? ctop[i] : 0;
         }
     }
     if (stamp) {

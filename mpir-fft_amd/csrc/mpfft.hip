@@ -57,6 +57,7 @@ struct Plan {
     int lbC, lbR;
     long j1, j2, trunc, Tr, len, total;
     int U, tpb, maxlogg;
+    int maxlogg_c;      // column passes (forward and inverse); maxlogg: row passes
     bool wave;          // wave-owned coefficient kernels (wkernels.hpp), l <= 512
     int wU;             // their limbs per lane
     bool wfull;         // l == 64 wU
@@ -135,8 +136,11 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
         int lg = 1;
         while (lg < BP_MAXLOGG && bp_lds_need(p->l, 2 << lg) <= BP_LDS_MAX) ++lg;
         p->maxlogg = lg;
+        // columns: two 74 KB groups per CU beat one 147 KB group at l = 2048 (C3 sweep,
+        // profiles/r02/sweep_blogg.txt: columns 5.97 ms vs 6.53 ms; rows 4.71 vs 4.44)
+        p->maxlogg_c = lg >= 3 ? lg - 1 : lg;
         const char *e = getenv("MPFFT_BLOGG");
-        if (e && atoi(e) >= 1 && atoi(e) <= lg) p->maxlogg = atoi(e);
+        if (e && atoi(e) >= 1 && atoi(e) <= lg) p->maxlogg = p->maxlogg_c = atoi(e);
     }
     p->slots = (size_t)2 * p->n;
     size_t o = 0;
@@ -240,9 +244,10 @@ struct Exec {
 
     // levels in the next pass when `rem` remain: the fewest passes of <= maxlogg
     // levels, balanced (C1 column inverse: 4 + 3 beats 5 + 2 by ~5 us)
-    int split(int rem) const
+    int split(int rem, bool col = false) const
     {
-        const int np = (rem + P.maxlogg - 1) / P.maxlogg;
+        const int ml = col && P.maxlogg_c ? P.maxlogg_c : P.maxlogg;
+        const int np = (rem + ml - 1) / ml;
         return (rem + np - 1) / np;
     }
 
@@ -423,7 +428,7 @@ struct Exec {
     {
         int lvl = 0;
         while (lvl < P.lbR) {
-            int k = split(P.lbR - lvl);
+            int k = split(P.lbR - lvl, true);
             PassArgs a = col_args();
             if (lvl == 0) {
                 a.src[0] = srcA; a.nsrc[0] = nA;
@@ -485,9 +490,32 @@ struct Exec {
             if (f) {
                 const size_t lds = pw_lds(M, 1 << lk, (int)P.l);
                 allow_lds((const void *)f, lds);
+                static const bool stamps = getenv("MPFFT_PW_STAMPS") != nullptr;
+                unsigned long long *dbg = nullptr;
+                if (stamps) {   // diagnostics only: per-workgroup phase stamps, averaged on the host
+                    HIPCHK(hipMalloc((void **)&dbg, (size_t)cnt * 64));
+                    HIPCHK(hipMemsetAsync(dbg, 0, (size_t)cnt * 64, s));
+                }
                 hipLaunchKernelGGL(f, dim3((unsigned)cnt), dim3(1u << lk), lds, s, row.dig[0], row.cb[0], row.top[0],
-                                   (const u64 *)row.dig[1], (const int *)row.top[1], (int)P.l, lk);
+                                   (const u64 *)row.dig[1], (const int *)row.top[1], (int)P.l, lk, dbg);
                 HIPCHK(hipGetLastError());
+                if (stamps) {
+                    unsigned long long *h = (unsigned long long *)malloc((size_t)cnt * 64);
+                    HIPCHK(hipMemcpyAsync(h, dbg, (size_t)cnt * 64, hipMemcpyDeviceToHost, s));
+                    HIPCHK(hipStreamSynchronize(s));
+                    double sum[8] = {0};
+                    long n = 0;
+                    for (long w = 0; w < cnt; ++w) {
+                        const unsigned long long *q = h + 8 * w;
+                        if (!q[7]) continue;
+                        ++n;
+                        for (int k = 1; k < 8; ++k) sum[k] += (double)(q[k] - q[k - 1]);
+                    }
+                    fprintf(stderr, "pw_stamps M=%d lk=%d slots=%ld/%ld: load %.0f fwdA %.0f fwdB %.0f mul %.0f inv %.0f final %.0f out %.0f\n",
+                            M, lk, n, cnt, sum[1] / n, sum[2] / n, sum[3] / n, sum[4] / n, sum[5] / n, sum[6] / n, sum[7] / n);
+                    free(h);
+                    (void)hipFree(dbg);
+                }
                 return MPFFT_OK;
             }
         }
@@ -568,7 +596,7 @@ struct Exec {
         const int lbM = ilog2(m);
         int hi = lbM;
         while (hi > 0) {
-            int k = split(hi);
+            int k = split(hi, true);
             PassArgs a = col_args();
             a.lbM = lbM;
             a.lvl0 = hi - k;

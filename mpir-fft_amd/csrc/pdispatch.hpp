@@ -3,7 +3,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
-typedef void (*pw_fn)(uint64_t *, uint64_t *, int *, const uint64_t *, const int *, int, int);
+typedef void (*pw_fn)(uint64_t *, uint64_t *, int *, const uint64_t *, const int *, int, int, unsigned long long *);
 
 pw_fn pw_get(int M);               // k_pwss<M> (M = inner coefficient limbs), nullptr if not built
 size_t pw_lds(int M, int K, int l);

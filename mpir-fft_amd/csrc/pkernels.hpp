@@ -36,31 +36,49 @@ __host__ __device__ constexpr size_t pw_lds_bytes(int M, int K, int l)
 //   2^E' x == U + (2^s - ov) - (1 + T) 2^(64 Y + s);  E >= N' negates (2^N' == -1).
 template <int M>
 __host__ __device__ __forceinline__ void pw_combine(u64 (&L)[M], int &T, int alpha, const u64 *X, const int *TT, int K,
-                                           int q, unsigned E)
+                                                   int q, unsigned E)
 {
     constexpr unsigned NP = 64 * M;
-    int sig = 1;
-    if (E >= NP) {
-        E -= NP;
-        sig = -1;
-    }
+    const bool neg = E >= NP;   // 2^N' == -1: subtract instead
+    if (neg) E -= NP;
     const int Y = (int)(E >> 6), s = (int)(E & 63);
-    const int Tq = TT[q];
-    i128 acc = 0;
-    if (alpha < 0) {   // -(L + T 2^N') = ~L + 1 + (-1 - T) 2^N'
+    const i64 Tq = TT[q];
+    i64 c = 0;                  // signed carry into the next limb
+    if (alpha < 0) {            // -(L + T 2^N') = ~L + 1 + (-1 - T) 2^N'
 #pragma unroll
         for (int j = 0; j < M; ++j) L[j] = ~L[j];
-        acc = 1;
+        c = 1;
         T = -1 - T;
     } else if (alpha == 0) {
 #pragma unroll
         for (int j = 0; j < M; ++j) L[j] = 0;
         T = 0;
     }
-    const u64 wtop = X[(M - 1 - Y) * K + q];              // W_(M-1), never wrapped (Y < M)
-    const u64 ov = (wtop >> 1) >> (63 - s);               // s == 0: 0
-    const i128 c0 = ((i128)1 << s) - (i128)ov;
-    const i128 cY = -(i128)(1 + Tq) * ((i128)1 << s);
+    // U = (W << s) + C0 at limb 0 + CY at limb Y (128-bit signed corrections, lo + hi 2^64)
+    const u64 wtop = X[(M - 1 - Y) * K + q];                  // W_(M-1), never wrapped (Y < M)
+    const u64 ov = (wtop >> 1) >> (63 - s);                   // the s bits shifted out (s == 0: 0)
+    u64 c0lo = ((u64)1 << s) - ov;                            // 2^s - ov in (0, 2^63]
+    i64 c0hi = 0;
+    const i64 v = -(1 + Tq);
+    u64 cylo = (u64)v << s;                                   // (1 + T) 2^s, negated
+    i64 cyhi = (v >> 1) >> (63 - s);
+    if (Y == 0) {   // both corrections at limb 0
+        const u64 t = c0lo + cylo;
+        c0hi += cyhi + (i64)(t < c0lo);
+        c0lo = t;
+        cylo = 0;
+        cyhi = 0;
+    }
+    u64 smask = 0;
+    if (neg) {      // -U = ~U + 1 - 2^N', corrections negated
+        smask = ~(u64)0;
+        c += 1;
+        T -= 1;
+        c0hi = -c0hi - (i64)(c0lo != 0);
+        c0lo = (u64)0 - c0lo;
+        cyhi = -cyhi - (i64)(cylo != 0);
+        cylo = (u64)0 - cylo;
+    }
     u64 wprev = 0;
 #pragma unroll
     for (int j = 0; j < M; ++j) {
@@ -69,17 +87,23 @@ __host__ __device__ __forceinline__ void pw_combine(u64 (&L)[M], int &T, int alp
         src += wr ? M : 0;
         u64 w = X[src * K + q];
         w = wr ? ~w : w;
-        const u64 u = (w << s) | ((wprev >> 1) >> (63 - s));
+        const u64 x = ((w << s) | ((wprev >> 1) >> (63 - s))) ^ smask;
         wprev = w;
-        i128 t = (i128)u;
-        if (j == 0) t += c0;
-        if (j == Y) t += cY;
-        acc += (i128)L[j];
-        acc += sig > 0 ? t : -t;
-        L[j] = (u64)acc;
-        acc >>= 64;
+        // L_j + x + c + correction, carry kept signed (|c| <= 4)
+        u64 r = L[j] + x;
+        i64 cy = (i64)(r < x);
+        const u64 r2 = r + (u64)c;
+        cy += c >= 0 ? (i64)(r2 < r) : -(i64)(r2 > r);
+        u64 cl = 0;
+        i64 ch = 0;
+        if (j == 0) { cl = c0lo; ch = c0hi; }
+        if (j == Y && j != 0) { cl = cylo; ch = cyhi; }
+        const u64 r3 = r2 + cl;
+        cy += (i64)(r3 < r2) + ch;
+        L[j] = r3;
+        c = cy;
     }
-    T += (int)(i64)acc;
+    T += (int)c;
 }
 
 // canonical residue of L + T 2^N' (== L - T): limbs in [0, 2^N'), returns 1 for 2^N' (L = 0)
@@ -134,47 +158,56 @@ __host__ __device__ __forceinline__ void pw_mulmod(u64 (&Z)[M], int &T, const u6
         T = -1 + (int)(i64)acc;
         return;
     }
-    // product scanning over 32-bit digits: digit c of (lo - hi), lo = digits [0, 2M), hi = [2M, 4M)
-    constexpr int D = 2 * M;
-    u32 a[D], b[D];
+    // Full product over 29-bit digits: a column sums at most ND < 64 products < 2^58,
+    // so one v_mad_u64_u32 per digit product with no carry tracking.  Columns are
+    // streamed into 64-bit limbs and folded on the fly: Z = lo - hi (2^N' == -1).
+    constexpr int DB = 29, ND = (64 * M + DB - 1) / DB;
+    static_assert(ND < 64, "column sums must stay below 2^64");
+    u32 ad[ND], bd[ND];
 #pragma unroll
-    for (int j = 0; j < M; ++j) {
-        a[2 * j] = (u32)La[j];
-        a[2 * j + 1] = (u32)(La[j] >> 32);
-        b[2 * j] = (u32)Lb[j];
-        b[2 * j + 1] = (u32)(Lb[j] >> 32);
-    }
-    i128 carry = 0;
-    u32 zd[D];
-#pragma unroll
-    for (int c = 0; c < D; ++c) {
-        u64 plo = 0, nlo = 0;
-        u32 phi = 0, nhi = 0;
-#pragma unroll
-        for (int i = 0; i <= c; ++i) {   // lo column c
-            const u64 pr = (u64)a[i] * b[c - i];
-            plo += pr;
-            phi += plo < pr;
+    for (int d = 0; d < ND; ++d) {
+        const int b0 = d * DB, li = b0 >> 6, sh = b0 & 63;
+        u64 x = La[li] >> sh, y = Lb[li] >> sh;
+        if (sh + DB > 64 && li + 1 < M) {
+            x |= La[li + 1] << (64 - sh);
+            y |= Lb[li + 1] << (64 - sh);
         }
+        ad[d] = (u32)(x & ((1u << DB) - 1));
+        bd[d] = (u32)(y & ((1u << DB) - 1));
+    }
+    u128 acc = 0;          // bits [pos, ...) of the product not yet emitted
+    int pos = 0, k = 0;    // compile-time after unrolling
+    i64 bw = 0;            // borrow of the lo - hi fold
+#pragma clang loop unroll(full)
+    for (int c = 0; c < 2 * ND - 1; ++c) {
+        u64 col = 0;
+        const int i0 = c < ND ? 0 : c - ND + 1, i1 = c < ND ? c : ND - 1;
+#pragma clang loop unroll(full)
+        for (int i = i0; i <= i1; ++i) col += (u64)ad[i] * bd[c - i];
+        acc += (u128)col << (DB * c - pos);
+        const bool last = c == 2 * ND - 2;
 #pragma unroll
-        for (int i = c + 1; i < D; ++i) {   // hi column c + D (wraps negated: 2^N' == -1)
-            const u64 pr = (u64)a[i] * b[c + D - i];
-            nlo += pr;
-            nhi += nlo < pr;
+        for (int e = 0; e < 3; ++e) {
+            if (k < 2 * M && (last || DB * (c + 1) - pos >= 64)) {
+                const u64 limb = (u64)acc;
+                acc >>= 64;
+                pos += 64;
+                if (k < M) {
+                    Z[k] = limb;
+                } else {                       // fold: Z[k - M] -= limb (borrow chain)
+                    const u64 z = Z[k - M];
+                    const u64 d1 = z - limb;
+                    i64 b1 = (i64)(d1 > z);
+                    const u64 d2 = d1 + (u64)bw;   // bw <= 0
+                    b1 += bw < 0 ? (i64)(d2 > d1) : 0;
+                    Z[k - M] = d2;
+                    bw = -b1;
+                }
+                ++k;
+            }
         }
-        carry += (i128)plo + ((i128)phi << 64) - (i128)nlo - ((i128)nhi << 64);
-        zd[c] = (u32)carry;
-        carry >>= 32;
     }
-    // value = Z + carry 2^N' == Z - carry, |carry| < 2^40: fold it so the top word stays small
-    i128 acc = -carry;
-#pragma unroll
-    for (int j = 0; j < M; ++j) {
-        acc += (i128)((u64)zd[2 * j] | ((u64)zd[2 * j + 1] << 32));
-        Z[j] = (u64)acc;
-        acc >>= 64;
-    }
-    T = (int)(i64)acc;   // in {-1, 0, 1}
+    T = (int)bw;   // value = Z + T 2^N', T in {-1, 0}
 }
 
 // exchange: thread t publishes its value (limbs L, top T) in the limb-major LDS buffer
@@ -229,8 +262,12 @@ __device__ __forceinline__ void pw_transform(u64 (&L)[M], int &T, unsigned &P, u
 // per slot; canonical inputs (limbs + carry limb in {0, 1}), reduced-form output.
 template <int M>
 __global__ __launch_bounds__(512) void k_pwss(u64 *digA, u64 *cbA, int *topA, const u64 *digB, const int *topB, int l,
-                                              int lk)
+                                              int lk, unsigned long long *dbg)
 {
+    // diagnostics (MPFFT_PW_STAMPS): thread 0 stamps the phase boundaries of this workgroup
+    unsigned long long *stamp = dbg ? dbg + 8 * (size_t)blockIdx.x : nullptr;
+#define PW_STAMP(k) do { if (stamp && threadIdx.x == 0) stamp[k] = __builtin_amdgcn_s_memtime(); } while (0)
+    PW_STAMP(0);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int K = 1 << lk, t = threadIdx.x;
     const int LP = l >> lk;                      // limbs per piece
@@ -269,8 +306,11 @@ __global__ __launch_bounds__(512) void k_pwss(u64 *digA, u64 *cbA, int *topA, co
         Lb[j] = j < LP ? pb[(size_t)t * LP + j] : 0;
     }
     unsigned Pa = (unsigned)(((u64)t * TH) % N2), Pb = Pa;   // negacyclic weight theta^t
+    PW_STAMP(1);
     pw_transform<M, 0>(La, Ta, Pa, X, TT, PP, lk, TH, t);
+    PW_STAMP(2);
     pw_transform<M, 0>(Lb, Tb, Pb, X, TT, PP, lk, TH, t);
+    PW_STAMP(3);
 
     // ---- inner products: 2^Pa xa * 2^Pb xb = 2^(Pa + Pb) (xa xb) ---------------------
     const int ca = pw_canon<M>(La, Ta), cb = pw_canon<M>(Lb, Tb);
@@ -278,9 +318,11 @@ __global__ __launch_bounds__(512) void k_pwss(u64 *digA, u64 *cbA, int *topA, co
     int Tz;
     pw_mulmod<M>(Z, Tz, La, ca, Lb, cb);
     unsigned Pz = (Pa + Pb) % N2;
+    PW_STAMP(4);
 
     // ---- inverse, then 2^-lk (division by K) and theta^-t --------------------------
     pw_transform<M, 1>(Z, Tz, Pz, X, TT, PP, lk, TH, t);
+    PW_STAMP(5);
     {
         const unsigned un = (unsigned)(((u64)t * TH + lk) % N2);
         const unsigned F = (Pz + N2 - un) % N2;
@@ -297,6 +339,7 @@ __global__ __launch_bounds__(512) void k_pwss(u64 *digA, u64 *cbA, int *topA, co
     X[(size_t)M * K + t] = (u64)zt;              // limb M of v (2^N' only)
     TT[t] = neg;
     __syncthreads();
+    PW_STAMP(6);
 
     // ---- combine: R = sum_t c_t 2^(B t) mod 2^N + 1 -------------------------------------
     // c_t 2^(Bt) = v_t 2^(Bt) - s_t (2^(Bt) + 2^(N' + Bt)); positions >= N wrap negated.
@@ -349,4 +392,9 @@ __global__ __launch_bounds__(512) void k_pwss(u64 *digA, u64 *cbA, int *topA, co
         }
     }
     if (t == 0) topA[slot] = 0;
+    if (stamp) {
+        __syncthreads();
+        PW_STAMP(7);
+    }
+#undef PW_STAMP
 }

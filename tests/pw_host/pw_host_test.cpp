@@ -19,7 +19,7 @@ template <int M> int run() {
     mpz_set_ui(p, 1); mpz_mul_2exp(p, p, 64 * M); mpz_add_ui(p, p, 1);
     int bad = 0;
     for (int it = 0; it < 20000; ++it) {
-        u64 L[M], X[M * K]; int T = (int)(rng() % 11) - 5, Tq = (int)(rng() % 11) - 5;
+        u64 L[M], X[M * K]; int T = (int)(rng() % 401) - 200, Tq = (int)(rng() % 401) - 200;
         for (int j = 0; j < M; ++j) L[j] = rng();
         int TT[K];
         for (int j = 0; j < M * K; ++j) X[j] = rng();
@@ -38,6 +38,8 @@ template <int M> int run() {
     for (int it = 0; it < 2000; ++it) {
         u64 La[M], Lb[M], Z[M]; int T;
         for (int j = 0; j < M; ++j) { La[j] = rng(); Lb[j] = rng(); }
+        if (it % 5 == 1) for (int j = 0; j < M; ++j) La[j] = Lb[j] = ~0ull;   // 2^N' - 1: every column at its maximum
+        if (it % 5 == 2) for (int j = 0; j < M; ++j) La[j] = ~0ull;
         int ta = it % 7 == 0, tb = it % 11 == 0;
         if (ta) for (int j = 0; j < M; ++j) La[j] = 0;
         if (tb) for (int j = 0; j < M; ++j) Lb[j] = 0;
