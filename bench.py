@@ -3,23 +3,35 @@
 
 A "step" is one full new_mpn_mul (split -> forward truncated MFA of both
 operands -> pointwise mulmod -> inverse MFA -> scale -> combine) of two
-synthetic operands already resident in HBM.  Default workload = BASELINE.json
-configs[1] (C1: depth 11, w 8, l = 256 limbs per coefficient, two 261952-limb
-operands).  value = (n1 + n2) * steps * world / max-rank time.
+synthetic operands already resident in HBM.  value = (n1 + n2) * steps / time.
 
-Multi-GPU (`--gpus N` under torch.distributed.run): every rank multiplies its
-own operand pair (independent products, no data-path collective; scaling
-"weak").  The column-sharded single-product path with the RCCL all-to-all is
-`--mode sharded` (see mpir-fft_amd/sharded.py).
+Workloads:
+  N = 1 (default): C3 -- 1.3e9-bit x 1.3e9-bit, depth 15, w 4, l = 2048 limbs per
+         coefficient, odd truncation point (BASELINE configs[3], the largest single-GPU
+         config); --config selects C0..C4 (C4 = 1e10 bits fits one MI355X too).
+  N > 1: C4 -- 1e10-bit operands, MFA columns sharded over the N ranks with RCCL
+         all-to-alls between the column and row passes (BASELINE configs[4],
+         mpir-fft_amd/sharded.py); "strong" scaling (one product split N ways).
+         `python bench.py --gpus N` with no torch.distributed environment launches
+         the N rank processes itself (torch.distributed.run, before any GPU call).
 
-Extra fields: "roofline" for the dominant kernel (time from HIP events on the
-library's stream inside the timed region), "stages" (per-stage ms), and
-"cpu_baseline": the oracle (oracle/, a CPU restatement of the reference,
-kind "port") timed on this host, rank 0 at N = 1 only.
+Fields beyond the driver contract:
+  roofline      the dominant kernel (largest stage time): algorithmic HBM bytes per
+                launch / its average duration from HIP events recorded inside the
+                timed region on the library's stream; traffic = FETCH+WRITE bytes per
+                launch from profiles/pmc_<config>.json (rocprofv3 --pmc, corrected as
+                MI355X_MICROARCH.md prescribes) when present.
+  pipeline      whole multiply vs the HBM roofline: B_alg = 8A + 16(n1+n2).
+  e2e_host      host-pointer new_mpn_mul (H2D + multiply + D2H), the drop-in boundary.
+  cpu_baseline  oracle/ (CPU restatement of the reference, kind "port", 1 thread) on
+                the same operands, plus GMP mpn_mul, CPU model and nproc (rank 0, N = 1).
 """
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -41,25 +53,14 @@ CONFIGS = {
 }
 SEED1, SEED2 = 0x1001, 0x2002
 
-STAGE_NAMES = ["fwd_columns", "fwd_rows", "pointwise", "inv_rows", "inv_columns", "scale", "combine"]
-STAGE_KERNEL = {"pointwise": "k_pwm (negacyclic products on v_mfma_i32_32x32x32_i8)", "scale": "k_scale",
-                "combine": "k_comb_sum + k_carry_*"}
-I8_MFMA_PEAK = 5.0e15      # int8 ops/s dense: 2x the 2.5 PF BF16 rate per clock (MI355X_MICROARCH.md)
-
-
-def pointwise_ops(P):
-    """Algorithmic int8 ops of one pointwise launch: T products of two 8l-byte numbers,
-    (8l)^2 byte MACs each, 2 ops per MAC (the schoolbook the int8 MFMA path executes)."""
-    return P["trunc"] * 2 * (8 * P["l"]) ** 2
-
 
 def stage_bytes(P, name, n1, n2):
-    """Algorithmic HBM bytes of one launch of a stage (DESIGN.md "Roofline accounting")."""
+    """Algorithmic HBM bytes of one multiply's stage (every launch of it together)."""
     T, l = P["trunc"], P["l"]
     blk = 8 * l + 4                         # one coefficient: l limbs + carry limb
-    if name == "fwd_columns":               # read operands, write 2 * T blocks
+    if name == "fwd_columns":               # read operands, write 2 T blocks
         return 8 * (n1 + n2) + 2 * T * blk
-    if name in ("fwd_rows",):
+    if name == "fwd_rows":                  # both operands in and out
         return 2 * 2 * T * blk
     if name == "pointwise":                 # read A, B, write A
         return 3 * T * blk
@@ -76,7 +77,18 @@ def b_alg(P, n1, n2):
     return 8 * A + 16 * (n1 + n2)
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(a, b, depth, w, budget_s):
+    """oracle/ new_mpn_mul (1 thread) on the bench operands; GMP mpn_mul beside it."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     reps, t0 = 0, time.perf_counter()
@@ -87,30 +99,85 @@ def cpu_baseline(a, b, depth, w, budget_s):
         el = time.perf_counter() - t0
         if el >= budget_s or reps >= 1000:
             break
-    return {"value": (len(a) + len(b)) * reps / el, "unit": "limbs/s", "cores": 1, "kind": "port",
-            "sample": f"{reps} full new_mpn_mul of the same operands via oracle/ (single thread), {el:.1f} s"}, ref
+    t1 = time.perf_counter()
+    g = O.gmp_mul(a, b)
+    tg = time.perf_counter() - t1
+    n = len(a) + len(b)
+    return {"value": n * reps / el, "unit": "limbs/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} full new_mpn_mul of the bench operands via oracle/ (CPU restatement of "
+                      f"mul_fft.c:3190, single thread), {el:.1f} s",
+            "gmp_mpn_mul_limbs_per_s": n / tg, "gmp_mpn_mul_s": tg,
+            "cpu_model": cpu_model(), "nproc": os.cpu_count()}, ref, g
 
 
-def pmc_traffic(cfg):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc summary, if any."""
+def pmc_traffic(cfg, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary of this config."""
     p = os.path.join(ROOT, "profiles", f"pmc_{cfg}.json")
-    if os.path.exists(p):
+    if not os.path.exists(p):
+        return None, None
+    with open(p) as f:
+        d = json.load(f)
+    for name, rec in d.get("kernels", {}).items():
+        if name.startswith(kernel.split(" ")[0].split("<")[0]) and "hbm_bytes_per_launch" in rec:
+            return rec["hbm_bytes_per_launch"], os.path.relpath(p, ROOT)
+    return None, None
+
+
+def golden_digest(cfg):
+    p = os.path.join(ROOT, "tests", "golden", "products.json")
+    try:
         with open(p) as f:
-            return json.load(f)
-    return None
+            return {c["name"]: c["sha256"] for c in json.load(f)}.get(cfg)
+    except OSError:
+        return None
+
+
+def launch_ranks(args):
+    """--gpus N without a torch.distributed environment: start N rank processes (no GPU
+    has been touched in this process) and return their exit status."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="C1", choices=sorted(CONFIGS))
-    ap.add_argument("--mode", default="replicas", choices=["replicas", "sharded"])
-    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline sampling")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS), help="default: C3 at N = 1, C4 at N > 1")
+    ap.add_argument("--mode", default=None, choices=["single", "replicas", "sharded"],
+                    help="N > 1: sharded (default) or independent replicas")
+    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of oracle sampling (>= 1 call)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--e2e-reps", type=int, default=2)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher/rendezvous check without a GPU: every rank joins a gloo group and "
+                         "rank 0 prints the world it saw (tests/test_bench_launcher.py)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    if args.dry_run:
+        import torch
+        import torch.distributed as dist
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        if world > 1:
+            dist.init_process_group("gloo")
+            t = torch.ones(1)
+            dist.all_reduce(t)
+            seen = int(t.item())
+            if dist.get_rank() == 0:
+                print(json.dumps({"n_gpus": world, "ranks_seen": seen, "dry_run": True}))
+            dist.destroy_process_group()
+        else:
+            print(json.dumps({"n_gpus": 1, "ranks_seen": 1, "dry_run": True}))
+        return
 
     import torch
     import torch.distributed as dist
@@ -120,24 +187,27 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    mode = args.mode or ("sharded" if world > 1 else "single")
+    cfg = args.config or ("C4" if world > 1 else "C3")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    if args.mode == "sharded":
+    if mode == "sharded":
         from importlib import import_module
         sh = import_module("mpir_fft_amd.sharded")
-        res = sh.bench(args, CONFIGS[args.config], rank, world, dev)
+        res = sh.bench(args, cfg, CONFIGS[cfg], rank, world, dev)
         if rank == 0:
             print(json.dumps(res))
         if world > 1:
             dist.destroy_process_group()
         return
 
-    depth, w, nl = CONFIGS[args.config]
+    depth, w, nl = CONFIGS[cfg]
     n1 = n2 = nl
     P = mp.plan_info(n1, n2, depth, w)
+    kern = mp.stage_kernels(n1, n2, depth, w)
     a = mp.fill_random(n1, SEED1 + 0x10000 * rank)
     b = mp.fill_random(n2, SEED2 + 0x10000 * rank)
     da = torch.from_numpy(a.view(np.int64)).to(dev)
@@ -146,58 +216,53 @@ def main():
     ws = mp.alloc_workspace(n1, n2, depth, w, dev)
     stream = torch.cuda.Stream(device=dev)
 
-    def step_full():
+    def step():
         mp.mul_device(dr, da, n1, db, n2, depth, w, ws, stream=stream)
 
-    def step(events=None):
-        for si, _ in enumerate(STAGE_NAMES):
-            if events is not None:
-                events[si].record(stream)
-            mp.stage(si, da, db, dr, n1, n2, depth, w, ws, stream=stream)
-        if events is not None:
-            events[len(STAGE_NAMES)].record(stream)
-
-    with torch.cuda.stream(stream):
-        for _ in range(args.warmup):
-            step_full()
+    for _ in range(args.warmup):
+        step()
     torch.cuda.synchronize(dev)
 
-    # timed region: K whole multiplies, one library call each (no per-stage events:
-    # an event record between two kernels costs ~5 us of idle GPU)
+    # timed region: K whole multiplies, one library call each; the library records a HIP
+    # event on its own stream at every stage boundary (mpfft_profile_begin), nothing else
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    mp.profile_begin(args.steps)
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step_full()
+    for _ in range(args.steps):
+        step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    stage_tot, calls = mp.profile_end()
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    stage_ms = {k: v / max(calls, 1) for k, v in stage_tot.items()}
 
-    # stage breakdown: the same K multiplies again, stage by stage, with HIP events
-    # recorded on the library's stream around every stage
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(STAGE_NAMES) + 1)] for _ in range(args.steps)]
-    torch.cuda.synchronize(dev)
-    for k in range(args.steps):
-        step(ev[k])
-    torch.cuda.synchronize(dev)
-    stage_ms = np.zeros(len(STAGE_NAMES))
-    for k in range(args.steps):
-        for si in range(len(STAGE_NAMES)):
-            stage_ms[si] += ev[k][si].elapsed_time(ev[k][si + 1])
-    stage_ms /= args.steps
-
+    got = dr.cpu().numpy().view(np.uint64)
     exact = None
     if not args.no_check and rank == 0:
-        got = dr.cpu().numpy().view(np.uint64)
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle as O
-        exact = bool((got == O.gmp_mul(a, b)).all())
+        want = golden_digest(cfg)
+        if want is not None:
+            exact = hashlib.sha256(got.tobytes()).hexdigest() == want
+
+    # end to end through the drop-in boundary (host pointers: H2D, multiply, D2H)
+    e2e = None
+    if args.e2e_reps > 0 and rank == 0:
+        r = np.zeros(n1 + n2, dtype=np.uint64)
+        mp.new_mpn_mul(r, a, n1, b, n2, depth, w)          # warm the host-pointer context
+        t1 = time.perf_counter()
+        for _ in range(args.e2e_reps):
+            mp.new_mpn_mul(r, a, n1, b, n2, depth, w)
+        te = (time.perf_counter() - t1) / args.e2e_reps
+        e2e = {"ms": te * 1e3, "limbs_per_s": (n1 + n2) / te, "same_product": bool((r == got).all()),
+               "note": "host arrays: H2D of both operands, the multiply, D2H of the product (PCIe included)"}
+        del r
+        mp.lib().mpfft_release()
 
     if rank != 0:
         if world > 1:
@@ -206,25 +271,17 @@ def main():
 
     ms_step = el / args.steps * 1e3
     value = world * (n1 + n2) * args.steps / el
-    dom = int(np.argmax(stage_ms))
-    dname = STAGE_NAMES[dom]
+    dname = max(stage_ms, key=stage_ms.get)
     dbytes = stage_bytes(P, dname, n1, n2)
-    achieved = dbytes / (stage_ms[dom] * 1e-3)
-    if dname == "pointwise" and P["l"] % 128 == 0:     # matrix-core kernel: priced against the int8 MFMA peak
-        ops = pointwise_ops(P)
-        roof = {"bound": "mfma", "achieved": ops / (stage_ms[dom] * 1e-3) / 1e12, "peak": I8_MFMA_PEAK / 1e12,
-                "unit": "TFLOP/s", "op_type": "int8 MAC ops (2 per MAC), TOP/s",
-                "frac": ops / (stage_ms[dom] * 1e-3) / I8_MFMA_PEAK, "alg_ops_per_launch": ops,
-                "hbm_achieved_GBps": achieved / 1e9, "alg_bytes_per_launch": dbytes}
-    else:
-        roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK, "alg_bytes_per_launch": dbytes}
-    pmc = pmc_traffic(args.config)
-    traffic = None
-    if pmc and pmc.get("stage") == dname:
-        traffic = pmc.get("hbm_bytes_per_launch")
+    dsec = stage_ms[dname] * 1e-3
+    traffic, traffic_src = pmc_traffic(cfg, kern[dname])
+    roof = {"bound": "hbm", "achieved": dbytes / dsec / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": dbytes / dsec / HBM_PEAK, "traffic": traffic, "traffic_source": traffic_src,
+            "kernel": kern[dname], "stage": dname, "avg_ms": stage_ms[dname],
+            "alg_bytes_per_launch": dbytes,
+            "timing": "HIP events on the library stream at the stage boundaries of the K timed multiplies"}
     balg = b_alg(P, n1, n2)
-    dev_ms = float(stage_ms.sum())
+    dev_ms = float(sum(stage_ms.values()))
     res = {
         "metric": METRIC,
         "value": value,
@@ -238,21 +295,23 @@ def main():
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic (xoshiro256** limbs, seeds 0x1001/0x2002 per rank)",
-        "config": {"workload": f"{args.config}: new_mpn_mul depth={depth} w={w} n1=n2={nl} limbs "
+        "config": {"workload": f"{cfg}: new_mpn_mul depth={depth} w={w} n1=n2={nl} limbs "
                                f"(l={P['l']} limbs/coeff, NC x NR = {P['NC']} x {P['NR']}, trunc={P['trunc']})",
                    "parallelism": f"replicas x{world}" if world > 1 else "single"},
-        "roofline": dict(roof, kernel=STAGE_KERNEL.get(dname, "k_lpass (" + dname + ")"), stage=dname,
-                         traffic=traffic, avg_ms=float(stage_ms[dom])),
-        "pipeline": {"device_ms": dev_ms, "b_alg_bytes": balg,
-                     "hbm_frac_b_alg": balg / (dev_ms * 1e-3) / HBM_PEAK},
-        "stages_ms": {n: float(t) for n, t in zip(STAGE_NAMES, stage_ms)},
-        "stage_timing": "separate K-multiply pass after the timed region, HIP events per stage on the library stream",
+        "roofline": roof,
+        "pipeline": {"device_ms": dev_ms, "b_alg_bytes": balg, "hbm_frac_b_alg": balg / (dev_ms * 1e-3) / HBM_PEAK,
+                     "note": "whole multiply vs the HBM roofline of the three-pass MFA (SURVEY 8d)"},
+        "stages_ms": stage_ms,
+        "stage_kernels": kern,
+        "e2e_host": e2e,
         "exact": exact,
+        "exact_check": "SHA-256 of the product limbs vs tests/golden/products.json (GMP mpn_mul)",
     }
     if world == 1 and not args.no_cpu_baseline:
-        cb, ref = cpu_baseline(a, b, depth, w, args.cpu_budget)
+        cb, ref, g = cpu_baseline(a, b, depth, w, args.cpu_budget)
         res["cpu_baseline"] = cb
-        res["exact_vs_port"] = bool((dr.cpu().numpy().view(np.uint64) == ref).all())
+        res["exact_vs_port"] = bool((got == ref).all())
+        res["exact_vs_gmp"] = bool((got == g).all())
     print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()

@@ -83,6 +83,7 @@ int mpfft_workspace_layout(long n1, long n2, unsigned long depth, unsigned long 
 #define MPFFT_STAGE_INV_COLUMNS 4   /* truncated column inverse                       (mul_fft.c:2959-2977) */
 #define MPFFT_STAGE_SCALE 5         /* divide by 2^(depth+1), normalise               (mul_fft.c:3256-3260) */
 #define MPFFT_STAGE_COMBINE 6       /* FFT_combine_bits                               (mul_fft.c:3261-3262) */
+#define MPFFT_NSTAGES 7
 int mpfft_stage(int stage, const uint64_t *d_i1, const uint64_t *d_i2, uint64_t *d_r, long n1, long n2,
                 unsigned long depth, unsigned long w, void *d_ws, size_t ws_bytes, void *stream);
 
@@ -120,6 +121,16 @@ size_t mpfft_shard_combine_tmp_bytes(long mcount);
 int mpfft_shard_combine(const mpfft_shard *sh, int phase, uint64_t *d_r, long m0, long mcount, long kbase,
                         const uint64_t *halo, int H, void *d_tmp, size_t tmp_bytes, int cin, int *d_sum,
                         void *stream);
+
+/* Stage profiling of the whole-multiply entries (new_mpn_mul, mpfft_mul_ex,
+ * mpfft_mul_device): between begin and end, each of the next max_calls multiplies
+ * records a HIP event on its own stream at every stage boundary (no other change to
+ * the work); end synchronises and returns the summed per-stage milliseconds
+ * (stage_ms[MPFFT_NSTAGES], MPFFT_STAGE_* order) and the number of profiled calls. */
+int mpfft_profile_begin(int max_calls);
+/* The kernel that carries each stage for these parameters, ';'-separated in MPFFT_STAGE_* order. */
+int mpfft_stage_kernels(long n1, long n2, unsigned long depth, unsigned long w, char *buf, size_t len);
+int mpfft_profile_end(float *stage_ms, int *calls);
 
 const char *mpfft_strerror(int code);
 int mpfft_version(void);

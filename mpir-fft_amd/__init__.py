@@ -65,6 +65,12 @@ def lib():
         h.new_mpn_mul.restype = None
         h.mpfft_mul_ex.argtypes = [_u64p, _u64p, _L, _u64p, _L, _UL, _UL]
         h.mpfft_mul_ex.restype = ctypes.c_int
+        h.mpfft_profile_begin.argtypes = [ctypes.c_int]
+        h.mpfft_profile_begin.restype = ctypes.c_int
+        h.mpfft_profile_end.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
+        h.mpfft_profile_end.restype = ctypes.c_int
+        h.mpfft_stage_kernels.argtypes = [_L, _L, _UL, _UL, ctypes.c_char_p, ctypes.c_size_t]
+        h.mpfft_stage_kernels.restype = ctypes.c_int
         h.mpfft_release.argtypes = []
         h.mpfft_release.restype = ctypes.c_int
         h.mpfft_mul_device.argtypes = [_vp, _vp, _L, _vp, _L, _UL, _UL, _vp, ctypes.c_size_t, _vp]
@@ -181,6 +187,35 @@ def stage(which, d_i1, d_i2, d_r, n1, n2, depth, w, ws, stream=None):
                            ws.numel() * ws.element_size(), _stream(stream))
     if rc:
         raise MpfftError(rc, f"mpfft_stage({which})")
+
+
+STAGE_NAMES = ("fwd_columns", "fwd_rows", "pointwise", "inv_rows", "inv_columns", "scale", "combine")
+
+
+def stage_kernels(n1, n2, depth, w):
+    """dict stage -> the kernel the library launches for it with these parameters"""
+    buf = ctypes.create_string_buffer(512)
+    rc = lib().mpfft_stage_kernels(n1, n2, depth, w, buf, len(buf))
+    if rc:
+        raise MpfftError(rc, "mpfft_stage_kernels")
+    return dict(zip(STAGE_NAMES, buf.value.decode().split(";")))
+
+
+def profile_begin(max_calls):
+    """Record HIP events at the stage boundaries of the next max_calls multiplies."""
+    rc = lib().mpfft_profile_begin(max_calls)
+    if rc:
+        raise MpfftError(rc, "mpfft_profile_begin")
+
+
+def profile_end():
+    """(dict stage -> summed ms, number of profiled multiplies); synchronises."""
+    ms = (ctypes.c_float * len(STAGE_NAMES))()
+    calls = ctypes.c_int(0)
+    rc = lib().mpfft_profile_end(ms, ctypes.byref(calls))
+    if rc:
+        raise MpfftError(rc, "mpfft_profile_end")
+    return dict(zip(STAGE_NAMES, [float(x) for x in ms])), calls.value
 
 
 def workspace_layout(n1, n2, depth, w):

@@ -468,6 +468,7 @@ struct Exec {
     }
 
     // nested negacyclic pointwise (pkernels.hpp) for big coefficients: (l -> pieces 2^lk)
+  public:
     static int pwss_lk(long l)
     {
         const char *e = getenv("MPFFT_PWSS");
@@ -801,26 +802,121 @@ struct Exec {
     }
 };
 
+// Stage profiling (mpfft_profile_begin/end): while active, run_all records a HIP event
+// on its own stream at every stage boundary of every multiply -- the timed calls are
+// otherwise unchanged -- and profile_end sums the per-stage times.
+struct StageProf {
+    bool on = false;
+    int cap = 0, used = 0;
+    hipEvent_t *ev = nullptr;   // cap * (MPFFT_NSTAGES + 1)
+};
+static std::mutex g_prof_mu;
+static StageProf g_prof;
+
+static void prof_mark(int call, int stage, hipStream_t s)
+{
+    if (call < 0) return;
+    (void)hipEventRecord(g_prof.ev[call * (MPFFT_NSTAGES + 1) + stage], s);
+}
+
 static int run_all(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, unsigned char *ws, hipStream_t s)
 {
     Exec X(P, s);
     X.single(ws);
     X.zflags = X.comb_flags(ws);
     X.zflags_n = X.comb_flag_words();
+    int call = -1;
+    {
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        if (g_prof.on && g_prof.used < g_prof.cap) call = g_prof.used++;
+    }
     int rc;
+    prof_mark(call, 0, s);
     if ((rc = X.fwd_columns(d_i1, P.n1, d_i2, P.n2, 2))) return rc;
+    prof_mark(call, 1, s);
     if ((rc = X.fwd_rows(2))) return rc;
+    prof_mark(call, 2, s);
     if ((rc = X.pointwise())) return rc;
+    prof_mark(call, 3, s);
     if ((rc = X.inv_rows())) return rc;
+    prof_mark(call, 4, s);
     if ((rc = X.itft(0, P.NR, P.Tr))) return rc;
+    prof_mark(call, 5, s);
     if ((rc = X.scale())) return rc;
-    return X.combine_single(d_r, ws);
+    prof_mark(call, 6, s);
+    rc = X.combine_single(d_r, ws);
+    prof_mark(call, 7, s);
+    return rc;
 }
 
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
 extern "C" {
+
+// Which kernel carries each stage for these parameters (the same decisions Exec makes).
+int mpfft_stage_kernels(long n1, long n2, unsigned long depth, unsigned long w, char *buf, size_t len)
+{
+    Plan P;
+    int rc = make_plan(&P, n1, n2, depth, w);
+    if (rc) return rc;
+    const char *pass = P.big ? "k_bpass" : (P.wave && P.lds) ? "k_lpass" : P.wave ? "k_wpass" : "k_pass";
+    char pw[64];
+    const int lk = Exec::pwss_lk(P.l);
+    if (lk && pw_get(pw_inner_limbs(P.l, lk)))
+        snprintf(pw, sizeof pw, "k_pwss<%d> (nested negacyclic, K=%d)", pw_inner_limbs(P.l, lk), 1 << lk);
+    else if (P.l % 256 == 0 && P.l <= 4096 && pw_kind() == 0)
+        snprintf(pw, sizeof pw, "k_pwm2 (int8 MFMA)");
+    else if (P.l % 128 == 0 && pw_kind() != 1)
+        snprintf(pw, sizeof pw, "k_pwm (int8 MFMA)");
+    else if (P.l % 2 == 0 && P.l >= 32)
+        snprintf(pw, sizeof pw, "k_pw (VALU)");
+    else
+        snprintf(pw, sizeof pw, "k_pointwise (VALU)");
+    const char *pair = P.wave ? "k_wpair" : "k_pairop";
+    const char *scale = P.fuse_scale ? "(fused into the last inverse column pass)" : P.wave ? "k_wscale" : "k_scale";
+    static const bool multi = [] { const char *e = getenv("MPFFT_COMBINE"); return e && !strcmp(e, "multi"); }();
+    snprintf(buf, len, "%s;%s;%s;%s;%s + %s;%s;%s", pass, pass, pw, pass, pass, pair, scale,
+             multi ? "k_comb_sum + k_carry_*" : "k_combine1");
+    return MPFFT_OK;
+}
+
+int mpfft_profile_begin(int max_calls)
+{
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    if (max_calls < 1) return MPFFT_EINVAL;
+    const int need = max_calls * (MPFFT_NSTAGES + 1);
+    if (g_prof.cap < max_calls) {
+        for (int i = 0; i < g_prof.cap * (MPFFT_NSTAGES + 1); ++i) (void)hipEventDestroy(g_prof.ev[i]);
+        free(g_prof.ev);
+        g_prof.ev = (hipEvent_t *)calloc((size_t)need, sizeof(hipEvent_t));
+        g_prof.cap = 0;
+        for (int i = 0; i < need; ++i)
+            if (hipEventCreate(&g_prof.ev[i]) != hipSuccess) return MPFFT_EHIP;
+        g_prof.cap = max_calls;
+    }
+    g_prof.used = 0;
+    g_prof.on = true;
+    return MPFFT_OK;
+}
+
+int mpfft_profile_end(float *stage_ms, int *calls)
+{
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof.on = false;
+    for (int k = 0; k < MPFFT_NSTAGES; ++k) stage_ms[k] = 0.f;
+    for (int c = 0; c < g_prof.used; ++c) {
+        hipEvent_t *e = g_prof.ev + c * (MPFFT_NSTAGES + 1);
+        if (hipEventSynchronize(e[MPFFT_NSTAGES]) != hipSuccess) return MPFFT_EHIP;
+        for (int k = 0; k < MPFFT_NSTAGES; ++k) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, e[k], e[k + 1]) != hipSuccess) return MPFFT_EHIP;
+            stage_ms[k] += ms;
+        }
+    }
+    if (calls) *calls = g_prof.used;
+    return MPFFT_OK;
+}
 
 const char *mpfft_strerror(int code)
 {

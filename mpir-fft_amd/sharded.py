@@ -213,9 +213,12 @@ class GpuBackend:
         return self._r
 
 
-def bench(args, cfg, rank, world, dev):
-    """`bench.py --mode sharded`: one multiply of config `cfg` split over all ranks."""
-    import json  # noqa: F401
+def bench(args, cfg_name, cfg, rank, world, dev):
+    """`bench.py --gpus N` (N > 1) / `--mode sharded`: one multiply of `cfg` split over
+    all ranks (strong scaling).  Returns rank 0's JSON record (driver contract fields)."""
+    import hashlib
+    import json
+    import os
     import time
 
     import torch
@@ -229,8 +232,8 @@ def bench(args, cfg, rank, world, dev):
     da = torch.from_numpy(a.view(np.int64)).to(dev)
     db = torch.from_numpy(b.view(np.int64)).to(dev)
     be = GpuBackend(mp, plan, dev)
-    comm = TorchComm(host_staging=(world > 1 and not dist.get_backend() == "nccl")) if world > 1 else None
-    job = ShardedMul(plan, rank, be, comm if comm else _SoloComm())
+    comm = TorchComm(host_staging=(world > 1 and dist.get_backend() != "nccl")) if world > 1 else _SoloComm()
+    job = ShardedMul(plan, rank, be, comm)
     for _ in range(args.warmup):
         job.run(da, db)
     torch.cuda.synchronize(dev)
@@ -247,12 +250,44 @@ def bench(args, cfg, rank, world, dev):
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    # exactness: rank 0 gathers the limb ranges in rank order and hashes them (golden digest)
+    exact = None
+    if not getattr(args, "no_check", False):
+        gpu_comm = world > 1 and dist.get_backend() == "nccl"
+        if rank == 0:
+            parts = [limbs.cpu().numpy().view(np.uint64)]
+            for d in range(1, world):
+                buf = torch.empty(plan.M[d + 1] - plan.M[d], dtype=torch.int64, device=dev if gpu_comm else "cpu")
+                dist.recv(buf, src=d)
+                parts.append(buf.cpu().numpy().view(np.uint64))
+            h = hashlib.sha256()
+            for p_ in parts:
+                h.update(p_.tobytes())
+            gp = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
+                              "products.json")
+            try:
+                want = {c["name"]: c["sha256"] for c in json.load(open(gp))}.get(cfg_name)
+                exact = h.hexdigest() == want if want else None
+            except OSError:
+                exact = None
+        elif world > 1:
+            dist.send(limbs if gpu_comm else limbs.cpu(), dst=0)
+    P = mp.plan_info(nl, nl, depth, w)
+    A = P["trunc"] * (P["l"] + 1) * 8
+    balg = 8 * A + 32 * nl
     return {"metric": "limbs/s for new_mpn_mul N×N-bit at 1/2/4/8 MI355X; % HBM roofline",
             "value": 2 * nl * args.steps / el, "unit": "limbs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-            "config": {"workload": f"sharded new_mpn_mul depth={depth} w={w} n1=n2={nl}",
-                       "parallelism": f"MFA columns x{world}, 3 all-to-all"}}
+            "scaling": "strong", "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic (xoshiro256** limbs, seeds 0x1001/0x2002)",
+            "config": {"workload": f"{cfg_name}: sharded new_mpn_mul depth={depth} w={w} n1=n2={nl} limbs "
+                                   f"(l={P['l']}, NC x NR = {P['NC']} x {P['NR']}, trunc={P['trunc']})",
+                       "parallelism": f"MFA columns x{world}, 3 all-to-all + halo all-gather "
+                                      f"({'RCCL' if world > 1 and dist.get_backend() == 'nccl' else 'local'})"},
+            "pipeline": {"b_alg_bytes": balg,
+                         "hbm_frac_b_alg": balg / (el / args.steps) / (world * 8.0e12),
+                         "note": "whole multiply vs the aggregate HBM roofline of the ranks (SURVEY 8d)"},
+            "exact": exact}
 
 
 class _SoloComm:
