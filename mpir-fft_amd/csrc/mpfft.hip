@@ -487,7 +487,7 @@ struct Exec {
         if (cnt == 0) return MPFFT_OK;
         if (const int lk = pwss_lk(P.l)) {
             const int M = pw_inner_limbs(P.l, lk);
-            pw_fn f = pw_get(M);
+            pw_fn f = pw_get(M, lk);
             if (f) {
                 const size_t lds = pw_lds(M, 1 << lk, (int)P.l);
                 allow_lds((const void *)f, lds);
@@ -863,7 +863,7 @@ int mpfft_stage_kernels(long n1, long n2, unsigned long depth, unsigned long w, 
     const char *pass = P.big ? "k_bpass" : (P.wave && P.lds) ? "k_lpass" : P.wave ? "k_wpass" : "k_pass";
     char pw[64];
     const int lk = Exec::pwss_lk(P.l);
-    if (lk && pw_get(pw_inner_limbs(P.l, lk)))
+    if (lk && pw_get(pw_inner_limbs(P.l, lk), lk))
         snprintf(pw, sizeof pw, "k_pwss<%d> (nested negacyclic, K=%d)", pw_inner_limbs(P.l, lk), 1 << lk);
     else if (P.l % 256 == 0 && P.l <= 4096 && pw_kind() == 0)
         snprintf(pw, sizeof pw, "k_pwm2 (int8 MFMA)");

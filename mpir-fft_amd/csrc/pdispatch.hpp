@@ -5,7 +5,7 @@
 
 typedef void (*pw_fn)(uint64_t *, uint64_t *, int *, const uint64_t *, const int *, int, int, unsigned long long *);
 
-pw_fn pw_get(int M);               // k_pwss<M> (M = inner coefficient limbs), nullptr if not built
+pw_fn pw_get(int M, int lk);       // k_pwss<M, lk> (M = inner coefficient limbs, 2^lk pieces), nullptr if not built
 size_t pw_lds(int M, int K, int l);
 
 // Inner ring for a product mod 2^(64 l) + 1 cut into K = 2^lk pieces: the smallest M

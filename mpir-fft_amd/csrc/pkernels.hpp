@@ -29,81 +29,99 @@ __host__ __device__ constexpr size_t pw_lds_bytes(int M, int K, int l)
     return (size_t)(M + 1) * K * 8 + (size_t)K * 8 + (size_t)l * 4;
 }
 
-// r = alpha * own + 2^E * x_q  (mod p', not reduced); alpha in {-1, 0, 1}.
-// x_q: limbs X[i K + q], top TT[q].  Derivation (E' = E mod N' = 64 Y + s):
-//   2^(64 Y) x == W + 1 - (1 + T) 2^(64 Y),  W_j = X_(j-Y) (j >= Y), ~X_(j-Y+M) (j < Y)
-//   2^s W == U - ov,  U = W << s (M limbs), ov = the s bits shifted out of the top
-//   2^E' x == U + (2^s - ov) - (1 + T) 2^(64 Y + s);  E >= N' negates (2^N' == -1).
+// Exchange format: thread t publishes its value as 2M 32-bit words, word k at
+// Xw[k K + t] (conflict-free for any rotation), top in TT[t].  Before publishing,
+// pw_norm moves the top to -1 (almost always exactly): the reader's rotation then
+// needs no correction term, only a complement mask and one carry chain.
+
+// L + T 2^N' == (L - (T + 1)) - 2^N'  (mod p'): subtract D = T + 1; returns the new top
+// (-1 unless the subtraction left [0, 2^N'), which needs L < D or L - D >= 2^N').
 template <int M>
-__host__ __device__ __forceinline__ void pw_combine(u64 (&L)[M], int &T, int alpha, const u64 *X, const int *TT, int K,
-                                                   int q, unsigned E)
+__host__ __device__ __forceinline__ int pw_norm(u64 (&L)[M], int T)
 {
-    constexpr unsigned NP = 64 * M;
-    const bool neg = E >= NP;   // 2^N' == -1: subtract instead
-    if (neg) E -= NP;
-    const int Y = (int)(E >> 6), s = (int)(E & 63);
-    const i64 Tq = TT[q];
-    i64 c = 0;                  // signed carry into the next limb
-    if (alpha < 0) {            // -(L + T 2^N') = ~L + 1 + (-1 - T) 2^N'
+    const int D = T + 1;
+    const u32 dh = D < 0 ? ~0u : 0u;
+    u32 b = 0;
 #pragma unroll
-        for (int j = 0; j < M; ++j) L[j] = ~L[j];
-        c = 1;
-        T = -1 - T;
-    } else if (alpha == 0) {
+    for (int j = 0; j < M; ++j) {
+        const u32 lo = __builtin_subc((u32)L[j], j == 0 ? (u32)D : dh, b, &b);
+        const u32 hi = __builtin_subc((u32)(L[j] >> 32), dh, b, &b);
+        L[j] = ((u64)hi << 32) | lo;
+    }
+    // L - D = L' + ((D < 0) - b) 2^N'
+    return (D < 0) - (int)b - 1;
+}
+
+// Values are kept with a sign flag S: the represented value is (-1)^S (L + T 2^N'), so
+// a butterfly's "-own" is a flag flip and every combine is own + (+-) rotated partner,
+// the partner's sign folded into the complement mask.
+// r = alpha * own + 2^E * x_q  (mod p', not reduced); alpha in {-1, 0, 1}.
+// x_q: words Xw[k K + q], TT[q] = 2 T_q + S_q.  With E' = E mod N' = 32 Yw + s5, s5 in [1, 32]:
+//   out = the N'-bit circular rotation of x_q's limbs by E', its low E' (wrapped) bits
+//         complemented:  out_k = alignbit(w_k, w_(k-1), 32 - s5),
+//         w_i = Xw[(i - Yw) mod 2M], complemented when i < Yw (i in [-1, 2M));
+//   2^E' x_q == out + 1 - (1 + T_q) 2^E'   (rotation wraps negated; T_q 2^N' == -T_q);
+//   negated (E >= N', or the signs differ):  ~out + 1 + (1 + T_q) 2^E'.
+// After pw_norm T_q = -1, so the (1 + T_q) term is a rare branch, and the whole sum is
+// one add-with-carry chain with carry-in 1.
+template <int M, int LK>
+__host__ __device__ __forceinline__ void pw_combine(u64 (&L)[M], int &T, int &S, int alpha, const u32 *Xw,
+                                                   const int *TT, int q, unsigned E)
+{
+    constexpr int K = 1 << LK, NW = 2 * M;
+    constexpr unsigned NP = 64 * M;
+    const int packed = TT[q], Tq = packed >> 1, Sq = packed & 1;
+    bool neg = E >= NP;
+    if (neg) E -= NP;
+    const int Yw = ((int)E - 1) >> 5;                    // E = 0: Yw = -1, s5 = 32
+    const unsigned sh = (unsigned)(32 * (Yw + 1)) - E;   // 32 - s5, in [0, 31]
+    if (alpha == 0) {
 #pragma unroll
         for (int j = 0; j < M; ++j) L[j] = 0;
         T = 0;
+        S = 0;
+    } else if (alpha < 0) {
+        S ^= 1;
     }
-    // U = (W << s) + C0 at limb 0 + CY at limb Y (128-bit signed corrections, lo + hi 2^64)
-    const u64 wtop = X[(M - 1 - Y) * K + q];                  // W_(M-1), never wrapped (Y < M)
-    const u64 ov = (wtop >> 1) >> (63 - s);                   // the s bits shifted out (s == 0: 0)
-    u64 c0lo = ((u64)1 << s) - ov;                            // 2^s - ov in (0, 2^63]
-    i64 c0hi = 0;
-    const i64 v = -(1 + Tq);
-    u64 cylo = (u64)v << s;                                   // (1 + T) 2^s, negated
-    i64 cyhi = (v >> 1) >> (63 - s);
-    if (Y == 0) {   // both corrections at limb 0
-        const u64 t = c0lo + cylo;
-        c0hi += cyhi + (i64)(t < c0lo);
-        c0lo = t;
-        cylo = 0;
-        cyhi = 0;
-    }
-    u64 smask = 0;
-    if (neg) {      // -U = ~U + 1 - 2^N', corrections negated
-        smask = ~(u64)0;
-        c += 1;
-        T -= 1;
-        c0hi = -c0hi - (i64)(c0lo != 0);
-        c0lo = (u64)0 - c0lo;
-        cyhi = -cyhi - (i64)(cylo != 0);
-        cylo = (u64)0 - cylo;
-    }
-    u64 wprev = 0;
+    neg ^= (S ^ Sq) != 0;
+    const u32 smask = neg ? ~0u : 0u;
+    const u32 *bn = Xw + q - Yw * K;          // source word i >= Yw: bn[i K]
+    const u32 *bw = bn + NW * K;              // i < Yw: wrapped
+    // w_(-1): wrapped unless Yw = -1 (then it is word 0 and the funnel shift is 0).
+    // Yw = -1 also reads row 2M at k = 2M - 1 (unused by the funnel): the buffer has it.
+    u32 wprev = (-1 < Yw ? bw : bn)[-K] ^ (-1 < Yw ? ~smask : smask);
+    u32 c = 1;
 #pragma unroll
-    for (int j = 0; j < M; ++j) {
-        int src = j - Y;
-        const bool wr = src < 0;
-        src += wr ? M : 0;
-        u64 w = X[src * K + q];
-        w = wr ? ~w : w;
-        const u64 x = ((w << s) | ((wprev >> 1) >> (63 - s))) ^ smask;
+    for (int k = 0; k < NW; ++k) {
+        const bool wr = k < Yw;
+        const u32 w = (wr ? bw : bn)[k * K] ^ (wr ? ~smask : smask);
+#if defined(__HIP_DEVICE_COMPILE__)
+        const u32 o = __builtin_amdgcn_alignbit(w, wprev, sh);
+#else
+        const u32 o = (u32)((((u64)w << 32) | wprev) >> sh);
+#endif
         wprev = w;
-        // L_j + x + c + correction, carry kept signed (|c| <= 4)
-        u64 r = L[j] + x;
-        i64 cy = (i64)(r < x);
-        const u64 r2 = r + (u64)c;
-        cy += c >= 0 ? (i64)(r2 < r) : -(i64)(r2 > r);
-        u64 cl = 0;
-        i64 ch = 0;
-        if (j == 0) { cl = c0lo; ch = c0hi; }
-        if (j == Y && j != 0) { cl = cylo; ch = cyhi; }
-        const u64 r3 = r2 + cl;
-        cy += (i64)(r3 < r2) + ch;
-        L[j] = r3;
-        c = cy;
+        const u32 lw = (u32)(L[k >> 1] >> (32 * (k & 1)));
+        const u32 r = __builtin_addc(lw, o, c, &c);
+        if (k & 1) L[k >> 1] = (L[k >> 1] & 0xffffffffull) | ((u64)r << 32);
+        else L[k >> 1] = (L[k >> 1] & ~0xffffffffull) | r;
     }
     T += (int)c;
+    if (Tq != -1) {   // rare: add cv 2^E', cv = -(1 + T_q) (negated when E >= N')
+        const int cv = neg ? 1 + Tq : -1 - Tq;
+        const i64 d = (i64)cv * ((i64)1 << (32 - sh));
+        const u32 dl = (u32)d, dhi = (u32)((u64)d >> 32), sx = d < 0 ? ~0u : 0u;
+        u32 cc = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            const u32 ad = k < Yw ? 0u : k == Yw ? dl : k == Yw + 1 ? dhi : sx;
+            const u32 lw = (u32)(L[k >> 1] >> (32 * (k & 1)));
+            const u32 r = __builtin_addc(lw, ad, cc, &cc);
+            if (k & 1) L[k >> 1] = (L[k >> 1] & 0xffffffffull) | ((u64)r << 32);
+            else L[k >> 1] = (L[k >> 1] & ~0xffffffffull) | r;
+        }
+        T += (int)cc + (Yw == NW - 1 ? (int)(d >> 32) : (d < 0 ? -1 : 0));
+    }
 }
 
 // canonical residue of L + T 2^N' (== L - T): limbs in [0, 2^N'), returns 1 for 2^N' (L = 0)
@@ -210,49 +228,60 @@ __host__ __device__ __forceinline__ void pw_mulmod(u64 (&Z)[M], int &T, const u6
     T = (int)bw;   // value = Z + T 2^N', T in {-1, 0}
 }
 
-// exchange: thread t publishes its value (limbs L, top T) in the limb-major LDS buffer
-template <int M>
-__device__ __forceinline__ void pw_publish(const u64 (&L)[M], int T, u64 *X, int *TT, int K, int t)
+// exchange: thread t normalises its value (pw_norm) and publishes it as words + top
+template <int M, int LK>
+__device__ __forceinline__ void pw_publish(u64 (&L)[M], int &T, int S, u32 *Xw, int *TT, int t)
 {
+    constexpr int K = 1 << LK;
+    T = pw_norm<M>(L, T);
 #pragma unroll
-    for (int j = 0; j < M; ++j) X[j * K + t] = L[j];
-    TT[t] = T;
+    for (int j = 0; j < M; ++j) {
+        Xw[(2 * j) * K + t] = (u32)L[j];
+        Xw[(2 * j + 1) * K + t] = (u32)(L[j] >> 32);
+    }
+    TT[t] = 2 * T + S;
 }
 
 // One forward (DIF) or inverse (DIT) length-K cyclic transform with root 2^(2 TH) over
 // the values of the K threads of this workgroup.  P: this thread's pending exponent.
-template <int M, int DIR>
-__device__ __forceinline__ void pw_transform(u64 (&L)[M], int &T, unsigned &P, u64 *X, int *TT, unsigned *PP, int lk,
+// a mod n for a < 4n, without a division (every exponent here is a sum of a few reduced terms)
+__device__ __forceinline__ unsigned pw_mod(unsigned a, unsigned n)
+{
+    a = a >= 2 * n ? a - 2 * n : a;
+    return a >= n ? a - n : a;
+}
+
+template <int M, int LK, int DIR>
+__device__ __forceinline__ void pw_transform(u64 (&L)[M], int &T, int &S, unsigned &P, u32 *Xw, int *TT, unsigned *PP,
                                              unsigned TH, int t)
 {
-    const int K = 1 << lk;
+    constexpr int K = 1 << LK, lk = LK;
     constexpr unsigned N2 = 128 * M;
+    // the level twiddle unit (2 TH) << j, reduced once per level; tw = (qt mod h) * unit < 2N' * ...
     for (int jj = 0; jj < lk; ++jj) {
         const int j = DIR == 0 ? jj : lk - 1 - jj;   // DIF level index (DIT runs them backwards)
         const int h = K >> (j + 1);
         const int q = t ^ h;
         const bool top = !(t & h);
         const int qt = t & ~h;                       // top index of the pair
-        const unsigned tw = (unsigned)(((u64)(qt & (h - 1)) << j) * (2 * TH) % N2);
-        pw_publish<M>(L, T, X, TT, K, t);
+        // (qt mod h) 2^j < K/2, times 2 TH: below N' (= K TH): no reduction needed
+        const unsigned tw = (unsigned)((qt & (h - 1)) << j) * (2 * TH);
+        pw_publish<M, LK>(L, T, S, Xw, TT, t);
         PP[t] = P;
         __syncthreads();
         const unsigned Pq = PP[q];
         unsigned E;
-        int alpha;
         if (DIR == 0) {
             // top: X_t + X_q = 2^P (x_t + 2^(Pq-P) x_q); bottom: (X_q - X_t) w^tw = 2^(P+tw) (2^(Pq-P) x_q - x_t)
-            E = (Pq + N2 - P) % N2;
-            alpha = top ? 1 : -1;
-            pw_combine<M>(L, T, alpha, X, TT, K, q, E);
-            if (!top) P = (P + tw) % N2;
+            E = pw_mod(Pq + N2 - P, N2);
+            pw_combine<M, LK>(L, T, S, top ? 1 : -1, Xw, TT, q, E);
+            if (!top) P = pw_mod(P + tw, N2);
         } else {
             // top: Z_t + Z_q w^-tw = 2^P (z_t + 2^(Pq-tw-P) z_q)
             // bottom: Z_q - Z_t w^-tw = 2^(P-tw) (2^(Pq-P+tw) z_q - z_t)
-            E = top ? (Pq + 2 * N2 - tw - P) % N2 : (Pq + N2 - P + tw) % N2;
-            alpha = top ? 1 : -1;
-            pw_combine<M>(L, T, alpha, X, TT, K, q, E);
-            if (!top) P = (P + N2 - tw) % N2;
+            E = top ? pw_mod(Pq + 2 * N2 - tw - P, N2) : pw_mod(Pq + N2 - P + tw, N2);
+            pw_combine<M, LK>(L, T, S, top ? 1 : -1, Xw, TT, q, E);
+            if (!top) P = pw_mod(P + N2 - tw, N2);
         }
         __syncthreads();
     }
@@ -260,20 +289,22 @@ __device__ __forceinline__ void pw_transform(u64 (&L)[M], int &T, unsigned &P, u
 
 // k_pwss<M>: A[slot] <- A[slot] * B[slot] mod 2^N + 1, one workgroup of K = 2^lk threads
 // per slot; canonical inputs (limbs + carry limb in {0, 1}), reduced-form output.
-template <int M>
-__global__ __launch_bounds__(512) void k_pwss(u64 *digA, u64 *cbA, int *topA, const u64 *digB, const int *topB, int l,
-                                              int lk, unsigned long long *dbg)
+template <int M, int LK>
+__global__ __launch_bounds__(1 << LK) void k_pwss(u64 *digA, u64 *cbA, int *topA, const u64 *digB, const int *topB,
+                                                  int l, int lk_unused, unsigned long long *dbg)
 {
     // diagnostics (MPFFT_PW_STAMPS): thread 0 stamps the phase boundaries of this workgroup
     unsigned long long *stamp = dbg ? dbg + 8 * (size_t)blockIdx.x : nullptr;
 #define PW_STAMP(k) do { if (stamp && threadIdx.x == 0) stamp[k] = __builtin_amdgcn_s_memtime(); } while (0)
     PW_STAMP(0);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int K = 1 << lk, t = threadIdx.x;
+    constexpr int K = 1 << LK, lk = LK;
+    const int t = threadIdx.x;
     const int LP = l >> lk;                      // limbs per piece
     constexpr unsigned NP = 64 * M, N2 = 2 * NP;
     const unsigned TH = NP >> lk;                // theta = 2^TH
-    u64 *X = (u64 *)smem;                        // (M + 1) K limbs
+    u64 *X = (u64 *)smem;                        // (M + 1) K limbs (words 2M + 2 rows during the transforms)
+    u32 *Xw = (u32 *)smem;
     int *TT = (int *)(X + (size_t)(M + 1) * K);  // K
     unsigned *PP = (unsigned *)(TT + K);         // K
     int *H = (int *)(PP + K);                    // l
@@ -299,36 +330,36 @@ __global__ __launch_bounds__(512) void k_pwss(u64 *digA, u64 *cbA, int *topA, co
 
     // ---- pieces and forward transforms (A, then B held in registers) -----------------
     u64 La[M], Lb[M];
-    int Ta = 0, Tb = 0;
+    int Ta = 0, Tb = 0, Sa = 0, Sb = 0;   // tops, sign flags
 #pragma unroll
     for (int j = 0; j < M; ++j) {
         La[j] = j < LP ? pa[(size_t)t * LP + j] : 0;
         Lb[j] = j < LP ? pb[(size_t)t * LP + j] : 0;
     }
-    unsigned Pa = (unsigned)(((u64)t * TH) % N2), Pb = Pa;   // negacyclic weight theta^t
+    unsigned Pa = (unsigned)t * TH, Pb = Pa;   // negacyclic weight theta^t (t TH < N')
     PW_STAMP(1);
-    pw_transform<M, 0>(La, Ta, Pa, X, TT, PP, lk, TH, t);
+    pw_transform<M, LK, 0>(La, Ta, Sa, Pa, Xw, TT, PP, TH, t);
     PW_STAMP(2);
-    pw_transform<M, 0>(Lb, Tb, Pb, X, TT, PP, lk, TH, t);
+    pw_transform<M, LK, 0>(Lb, Tb, Sb, Pb, Xw, TT, PP, TH, t);
     PW_STAMP(3);
 
     // ---- inner products: 2^Pa xa * 2^Pb xb = 2^(Pa + Pb) (xa xb) ---------------------
     const int ca = pw_canon<M>(La, Ta), cb = pw_canon<M>(Lb, Tb);
     u64 Z[M];
-    int Tz;
+    int Tz, Sz = Sa ^ Sb;
     pw_mulmod<M>(Z, Tz, La, ca, Lb, cb);
-    unsigned Pz = (Pa + Pb) % N2;
+    unsigned Pz = pw_mod(Pa + Pb, N2);
     PW_STAMP(4);
 
     // ---- inverse, then 2^-lk (division by K) and theta^-t --------------------------
-    pw_transform<M, 1>(Z, Tz, Pz, X, TT, PP, lk, TH, t);
+    pw_transform<M, LK, 1>(Z, Tz, Sz, Pz, Xw, TT, PP, TH, t);
     PW_STAMP(5);
     {
-        const unsigned un = (unsigned)(((u64)t * TH + lk) % N2);
-        const unsigned F = (Pz + N2 - un) % N2;
-        pw_publish<M>(Z, Tz, X, TT, K, t);
+        const unsigned un = (unsigned)t * TH + lk;   // < N' + lk
+        const unsigned F = pw_mod(Pz + N2 - un, N2);
+        pw_publish<M, LK>(Z, Tz, Sz, Xw, TT, t);
         __syncthreads();
-        pw_combine<M>(Z, Tz, 0, X, TT, K, t, F);
+        pw_combine<M, LK>(Z, Tz, Sz, 0, Xw, TT, t, F);   // clears the sign flag
         __syncthreads();
     }
     // signed coefficient c_t = v - s p', v in [0, 2^N'], s = (v > 2^(N'-1))

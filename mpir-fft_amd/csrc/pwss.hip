@@ -2,13 +2,11 @@
 #include "pkernels.hpp"
 #include "pdispatch.hpp"
 
-pw_fn pw_get(int M)
+pw_fn pw_get(int M, int lk)
 {
-    switch (M) {
-    case 12: return k_pwss<12>;
-    case 20: return k_pwss<20>;
-    case 24: return k_pwss<24>;
-    }
+    if (M == 12 && lk == 8) return k_pwss<12, 8>;
+    if (M == 20 && lk == 8) return k_pwss<20, 8>;
+    if (M == 24 && lk == 9) return k_pwss<24, 9>;
     return nullptr;
 }
 

@@ -1,5 +1,5 @@
 // Host-side unit test of the nested-pointwise arithmetic (mpir-fft_amd/csrc/pkernels.hpp):
-// pw_combine (rotated add in R' = Z/(2^N'+1)), pw_mulmod (inner product) and pw_canon,
+// pw_norm + pw_combine (rotated add in R' = Z/(2^N'+1)), pw_mulmod (inner product) and pw_canon,
 // each against GMP mpz on random operands.  The same source runs on the GPU inside
 // k_pwss; these functions are __host__ __device__ so the CPU suite can pin them.
 // Built by __graft_entry__.build() (tests/pw_host/Makefile), run by tests/test_pw_host.py.
@@ -14,23 +14,32 @@ template <int M> void tovals(mpz_t z, const u64 *L, int T) {
     mpz_t t; mpz_init_set_si(t, T); mpz_mul_2exp(t, t, 64 * M); mpz_add(z, z, t); mpz_clear(t);
 }
 template <int M> int run() {
-    constexpr int K = 4;
+    constexpr int LK = 2, K = 1 << LK;
     mpz_t p, a, b, want, got, e2; mpz_inits(p, a, b, want, got, e2, NULL);
     mpz_set_ui(p, 1); mpz_mul_2exp(p, p, 64 * M); mpz_add_ui(p, p, 1);
     int bad = 0;
     for (int it = 0; it < 20000; ++it) {
-        u64 L[M], X[M * K]; int T = (int)(rng() % 401) - 200, Tq = (int)(rng() % 401) - 200;
-        for (int j = 0; j < M; ++j) L[j] = rng();
-        int TT[K];
-        for (int j = 0; j < M * K; ++j) X[j] = rng();
-        for (int j = 0; j < K; ++j) TT[j] = Tq;
-        int q = rng() % K; unsigned E = rng() % (128 * M); int alpha = (int)(rng() % 3) - 1;
-        u64 Xq[M]; for (int j = 0; j < M; ++j) Xq[j] = X[j * K + q];
-        tovals<M>(a, L, T); tovals<M>(b, Xq, Tq);
+        // own value (L, T); partner q published as words (pw_publish's layout, 2M + 2 rows)
+        u64 L[M], Lq[M]; int T = (int)(rng() % 401) - 200, Tq = (int)(rng() % 401) - 200;
+        for (int j = 0; j < M; ++j) { L[j] = rng(); Lq[j] = rng(); }
+        if (it % 7 == 3) for (int j = 0; j < M; ++j) Lq[j] = it % 2 ? 0 : ~0ull;   // pw_norm wraps
+        int q = rng() % K; unsigned E = it % 13 == 0 ? (unsigned)(rng() % 4) * 64 * M / 2 : rng() % (128 * M);
+        int alpha = (int)(rng() % 3) - 1, S = (int)(rng() & 1), Sq = (int)(rng() & 1);
+        tovals<M>(b, Lq, Tq);
+        if (it % 3) Tq = pw_norm<M>(Lq, Tq);   // the published form (top almost always -1)
+        u64 chk; { mpz_t c2; mpz_init(c2); tovals<M>(c2, Lq, Tq); mpz_sub(c2, c2, b); mpz_mod(c2, c2, p);
+                   chk = mpz_sgn(c2); mpz_clear(c2); }
+        if (chk) { if (bad++ < 5) printf("norm mismatch it=%d\n", it); }
+        u32 Xw[(2 * M + 2) * K]; int TT[K];
+        for (int j = 0; j < (2 * M + 2) * K; ++j) Xw[j] = (u32)rng();
+        for (int j = 0; j < M; ++j) { Xw[2 * j * K + q] = (u32)Lq[j]; Xw[(2 * j + 1) * K + q] = (u32)(Lq[j] >> 32); }
+        TT[q] = 2 * Tq + Sq;
+        // represented values carry a sign flag: (-1)^S (L + T 2^N')
+        tovals<M>(a, L, T); if (S) mpz_neg(a, a); if (Sq) mpz_neg(b, b);
         mpz_ui_pow_ui(e2, 2, E); mpz_mul(want, b, e2); mpz_mul_si(a, a, alpha); mpz_add(want, want, a); mpz_mod(want, want, p);
-        pw_combine<M>(L, T, alpha, X, TT, K, q, E);
-        tovals<M>(got, L, T); mpz_mod(got, got, p);
-        if (mpz_cmp(got, want)) { if (bad++ < 5) printf("combine mismatch it=%d E=%u alpha=%d\n", it, E, alpha); }
+        pw_combine<M, LK>(L, T, S, alpha, Xw, TT, q, E);
+        tovals<M>(got, L, T); if (S) mpz_neg(got, got); mpz_mod(got, got, p);
+        if (mpz_cmp(got, want)) { if (bad++ < 5) printf("combine mismatch it=%d E=%u alpha=%d Tq=%d\n", it, E, alpha, Tq); }
     }
     printf("M=%d combine bad=%d\n", M, bad);
     int bad0 = bad;
