@@ -31,6 +31,7 @@
 #include "wdispatch.hpp"
 #include "bdispatch.hpp"
 #include "pdispatch.hpp"
+#include "rdispatch.hpp"
 #include "../../include/mpfft.h"
 
 // ---------------------------------------------------------------------------
@@ -64,6 +65,7 @@ struct Plan {
     bool fuse_scale;    // scaling fused into the last inverse column pass (no truncation)
     bool lds;           // LDS-resident radix-2^5 passes (lkernels.hpp)
     bool big;           // LDS-resident passes for 512 <= l <= 4096 (bkernels.hpp)
+    bool rpass;         // register-resident passes (rkernels.hpp) where they apply, l = 1024, 2048, 4096
     size_t slots;       // allocated slots per operand
     size_t off_digA, off_topA, off_cbA, off_digB, off_topB, off_cbB, off_lo, off_hi, off_bg, off_bp, off_bc, bytes;
     long nblk;
@@ -141,6 +143,12 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
         p->maxlogg_c = lg >= 3 ? lg - 1 : lg;
         const char *e = getenv("MPFFT_BLOGG");
         if (e && atoi(e) >= 1 && atoi(e) <= lg) p->maxlogg = p->maxlogg_c = atoi(e);
+        const char *er = getenv("MPFFT_RPASS");
+        p->rpass = rp_maxlogg((int)p->l) > 0 && !(er && !strcmp(er, "0")) && !getenv("MPFFT_BP_STAMPS");
+        if (p->rpass && !e) {   // same levels per pass for columns and rows (two groups per CU either way)
+            const int rl = rp_maxlogg((int)p->l) < lg ? rp_maxlogg((int)p->l) : lg;
+            p->maxlogg = p->maxlogg_c = rl;
+        }
     }
     p->slots = (size_t)2 * p->n;
     size_t o = 0;
@@ -282,8 +290,40 @@ struct Exec {
         return (int)(fit < G ? fit : G);
     }
 
+    // k_rpass takes a pass unless it needs a canonical store, has zero inputs outside the
+    // split, or some level rotation is not a whole number of limb pairs
+    int rpass_mode(const PassArgs &a, int logg, int dir) const
+    {
+        if (!P.rpass || logg > rp_maxlogg((int)P.l) || a.canon || a.rho % 128) return -1;
+        if (dir == 0) {
+            if (a.scale_e || a.tw_mode == 2) return -1;
+            if (a.src[0] || a.src[1]) return a.tw_mode ? -1 : 2;
+            if (a.zero_from < (1 << a.lbM)) return -1;
+            return a.tw_mode == 1 ? 1 : 0;
+        }
+        if (a.tw_mode == 1) return -1;
+        return (a.tw_mode == 2 || a.scale_e) ? 1 : 0;
+    }
+
     int pass(PassArgs a, int logg, int dir, int nops)
     {
+        int rm = rpass_mode(a, logg, dir);
+        static const int rmask = [] { const char *e = getenv("MPFFT_RPASS_OFF"); return e ? atoi(e) : 0; }();
+        if (rm >= 0 && (rmask >> (3 * dir + rm) & 1)) rm = -1;   // diagnostics: bit 3 dir + mode off
+        if (rm >= 0) {
+            rp_fn f = rp_get((int)P.l, logg, dir, rm);
+            if (!f) return MPFFT_EUNSUPPORTED;
+            static const size_t pad = [] { const char *e = getenv("MPFFT_RPASS_LDSPAD"); return e ? (size_t)atol(e) : 0; }();
+            static const int abl = [] { const char *e = getenv("MPFFT_ABLATE"); return e ? atoi(e) : 0; }();
+            a.ablate = abl;
+            const size_t lds = rp_lds((int)P.l, logg) + pad;   // pad: diagnostics (one workgroup per CU)
+            allow_lds((const void *)f, lds);
+            a.ngroups = 1 << (a.lbM - logg);
+            dim3 grid((unsigned)((long)a.nsub * a.ngroups), (unsigned)nops);
+            hipLaunchKernelGGL(f, grid, dim3(RP_NT), lds, s, a);
+            HIPCHK(hipGetLastError());
+            return MPFFT_OK;
+        }
         if (P.big) {
             // limb-aligned kernel unless some rotation of the pass has a sub-limb part
             const bool gen = (a.rho % 64) || (a.tw_mode && a.tw_w % 64) || (a.scale_e % 64);
@@ -860,7 +900,8 @@ int mpfft_stage_kernels(long n1, long n2, unsigned long depth, unsigned long w, 
     Plan P;
     int rc = make_plan(&P, n1, n2, depth, w);
     if (rc) return rc;
-    const char *pass = P.big ? "k_bpass" : (P.wave && P.lds) ? "k_lpass" : P.wave ? "k_wpass" : "k_pass";
+    const char *pass = P.big ? (P.rpass ? "k_rpass" : "k_bpass") : (P.wave && P.lds) ? "k_lpass" : P.wave ? "k_wpass" : "k_pass";
+    const char *rows = P.big && P.rpass ? "k_rpass + k_bpass (canonical last pass)" : pass;
     char pw[64];
     const int lk = Exec::pwss_lk(P.l);
     if (lk && pw_get(pw_inner_limbs(P.l, lk), lk))
@@ -876,7 +917,7 @@ int mpfft_stage_kernels(long n1, long n2, unsigned long depth, unsigned long w, 
     const char *pair = P.wave ? "k_wpair" : "k_pairop";
     const char *scale = P.fuse_scale ? "(fused into the last inverse column pass)" : P.wave ? "k_wscale" : "k_scale";
     static const bool multi = [] { const char *e = getenv("MPFFT_COMBINE"); return e && !strcmp(e, "multi"); }();
-    snprintf(buf, len, "%s;%s;%s;%s;%s + %s;%s;%s", pass, pass, pw, pass, pass, pair, scale,
+    snprintf(buf, len, "%s;%s;%s;%s;%s + %s;%s;%s", pass, rows, pw, pass, pass, pair, scale,
              multi ? "k_comb_sum + k_carry_*" : "k_combine1");
     return MPFFT_OK;
 }

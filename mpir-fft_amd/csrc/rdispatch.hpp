@@ -1,0 +1,25 @@
+// rdispatch.hpp -- host-side view of the register-resident big-coefficient passes
+// (rkernels.hpp, rpass_p*.hip)
+#pragma once
+#include <stddef.h>
+
+struct PassArgs;
+typedef void (*rp_fn)(PassArgs);
+
+#define RP_NT 512   // threads per workgroup; two workgroups share a CU
+
+// k_rpass<LOGG, PP, DIR, MODE> for coefficients of l = 1024 PP limbs (PP = 1, 2, 4);
+// MODE: DIR 0: 1 = MFA twiddle applied on load, 2 = split fused into the load;
+//       DIR 1: 1 = general final multipliers (inverse twiddle, scaling).
+rp_fn rp_get(int l, int logg, int dir, int mode);
+
+// most levels per pass: G l <= 16384 limbs per workgroup (32 limbs per thread)
+inline int rp_maxlogg(int l) { return l == 1024 ? 3 : l == 2048 ? 3 : l == 4096 ? 2 : 0; }   // l = 1024: G = 16 spills
+
+// LDS: NX exchange slots of 9 l bytes (limbs + 16-bit pair overflows).  <= 73 728 B,
+// so two workgroups fit in 160 KiB.
+inline size_t rp_lds(int l, int logg)
+{
+    const int G = 1 << logg, NX = G / 2 > 2 ? G / 2 : 2;
+    return (size_t)NX * 9 * l;
+}

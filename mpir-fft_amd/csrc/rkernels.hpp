@@ -1,0 +1,470 @@
+// rkernels.hpp -- register-resident radix-2^LOGG passes for big coefficients
+// (l = 1024 PP limbs, PP = 1, 2, 4: the 10^9..10^10-bit configs C2-C4).
+//
+// Same work and HBM format as k_bpass (bkernels.hpp): one workgroup runs LOGG radix-2
+// levels of FFT_radix2_twiddle / FFT_radix2 / IFFT_radix2(_twiddle) (mul_fft.c:1397,
+// :786, :1444, :1964) on a butterfly group of G = 2^LOGG coefficients of one column or
+// row, with the MFA twiddles (README:89), the fused split (FFT_split_bits, :115) and
+// the fused 2^-(depth+1) scaling (:3256-3260).
+//
+// Why a second big-coefficient kernel: k_bpass keeps the group in LDS (G = 8 at
+// l = 2048 fills 147 KB), so one workgroup owns a CU and its HBM load, level and store
+// phases run back to back -- the stamps (MPFFT_BP_STAMPS) showed half of every group's
+// time waiting on the load.  Here the group lives in VGPRs: 512 threads, thread t owns
+// limb pairs pp = t + 512 r (r < PP) of every coefficient, 32 limbs per thread at most
+// (G PP <= 16), and LDS is only the exchange buffer for the rotations (<= 78 KB).  Two
+// workgroups share a CU, so one's loads and stores overlap the other's levels.
+//
+// Register form of a residue mod p = 2^N + 1: per limb pair (2q, 2q+1) two limbs and a
+// signed overflow count,  x = sum_q (a_q + b_q 2^64 + h_q 2^128) 2^(128 q)  (mod p).
+// A butterfly is a 128-bit add/sub per pair (the h absorb the carries, no chain across
+// pairs).  Multiplications by 2^e are deferred as in k_bpass (pending exponents, closed
+// forms of the slot index); for every pass this kernel takes, a level's relative
+// exponent is a whole number of limb *pairs* (host: rho % 128 == 0), so the partner is
+// read from LDS by a pair-index shift with a sign flip past 2^N.  The two exponents that
+// are not (the MFA twiddle before the row DIF, the inverse twiddle / scaling after the
+// row or column DIT) are applied once, by a general rotation through LDS on 32-bit
+// digits (rp_rot_all), right after the load or after the last level.
+//
+// HBM store: reduced form (limbs + carry masks, coeff.hpp): the pair overflow h_q is the
+// carry into limb 2q+2, one LDS exchange hands it to the thread owning that limb.
+#pragma once
+#include "bkernels.hpp"
+#include "rdispatch.hpp"
+
+typedef unsigned long long rp_v2u __attribute__((ext_vector_type(2)));
+
+// compiler-only memory barrier: keeps LDS reads from being hoisted en masse (each hoisted
+// read holds its VGPRs; the coefficients already take 80 of the 128)
+#define RP_FENCE() asm volatile("" ::: "memory")
+// diagnostics only (MPFFT_ABLATE & 1): a workgroup barrier wherever a phase could race
+#define RP_DBG_SYNC() do { if (a.ablate & 1) __syncthreads(); } while (0)
+
+struct Pr {
+    u64 a, b;   // limbs 2q, 2q+1
+    int h;      // overflow: weight 2^128 (into limb 2q+2; the last pair's weighs 2^N == -1)
+};
+
+__device__ __forceinline__ Pr pr_add(const Pr &x, const Pr &y)
+{
+    Pr r;
+    u64 t;
+    const bool c0 = __builtin_add_overflow(x.a, y.a, &r.a);
+    const bool c1 = __builtin_add_overflow(x.b, y.b, &t);
+    const bool c2 = __builtin_add_overflow(t, (u64)c0, &r.b);
+    r.h = x.h + y.h + (int)c1 + (int)c2;
+    return r;
+}
+
+__device__ __forceinline__ Pr pr_sub(const Pr &x, const Pr &y)
+{
+    Pr r;
+    u64 t;
+    const bool b0 = __builtin_sub_overflow(x.a, y.a, &r.a);
+    const bool b1 = __builtin_sub_overflow(x.b, y.b, &t);
+    const bool b2 = __builtin_sub_overflow(t, (u64)b0, &r.b);
+    r.h = x.h - y.h - (int)b1 - (int)b2;
+    return r;
+}
+
+// x +- y with the sign of y folded in: (x + s y, x - s y), s = -1 when neg
+__device__ __forceinline__ void pr_bfly(Pr &u, Pr &v, const Pr &x, const Pr &y, bool neg)
+{
+    const Pr p = pr_add(x, y), m = pr_sub(x, y);
+    u = neg ? m : p;
+    v = neg ? p : m;
+}
+
+// branch-free (the sign varies per lane): -x = (~x + 1) in the 128 bits, h -> -h - (x != 0)
+__device__ __forceinline__ Pr pr_cneg(const Pr &x, bool neg)
+{
+    const u64 m = neg ? MPF_MAXL : 0;
+    Pr r;
+    u64 t;
+    const bool c0 = __builtin_add_overflow(x.a ^ m, (u64)neg, &r.a);
+    const bool c1 = __builtin_add_overflow(x.b ^ m, (u64)c0, &t);
+    r.b = t;
+    r.h = (neg ? ~x.h : x.h) + (int)c1;
+    return r;
+}
+
+// exchange slot j: limbs (8 l bytes) then pair overflows (l/2 int16)
+template <int PP>
+struct RX {
+    static constexpr int l = 1024 * PP;
+    static constexpr size_t SB = (size_t)9 * l;
+    unsigned char *base;
+    __device__ __forceinline__ u64 *f(int j) const { return (u64 *)(base + (size_t)j * SB); }
+    __device__ __forceinline__ short *h(int j) const { return (short *)(base + (size_t)j * SB + 8 * (size_t)l); }
+};
+
+template <int PP>
+__device__ __forceinline__ void rp_pub(const RX<PP> &X, int j, const Pr (&x)[PP], int t)
+{
+#pragma unroll
+    for (int r = 0; r < PP; ++r) {
+        const int pp = t + RP_NT * r;
+        *(rp_v2u *)(X.f(j) + 2 * pp) = rp_v2u{x[r].a, x[r].b};
+        X.h(j)[pp] = (short)x[r].h;
+    }
+}
+
+// pair pp of 2^e y, y published in slot j; e a multiple of 128 bits (whole pairs), e < 2N.
+// Returns the pair unsigned; neg = its sign.
+template <int PP>
+__device__ __forceinline__ Pr rp_get_al(const RX<PP> &X, int j, int pp, u64 e, u64 N, bool &neg)
+{
+    constexpr int HP = RX<PP>::l / 2;
+    const bool sg = e >= N;
+    const int Yp = (int)((sg ? e - N : e) >> 7);
+    int src = pp - Yp;
+    const bool wr = src < 0;
+    src += wr ? HP : 0;
+    const rp_v2u v = *(const rp_v2u *)(X.f(j) + 2 * src);
+    Pr r;
+    r.a = v.x;
+    r.b = v.y;
+    r.h = X.h(j)[src];
+    neg = wr != sg;
+    return r;
+}
+
+// pair pp of 2^e y for any e < 2N (32-bit digit rotation, as bp_ld).  The 5 source digits
+// 4pp - y - 1 .. 4pp + 3 - y lie in 3 consecutive limbs m0 .. m0+2 (wrapped ones negated,
+// 2^N == -1); the low digit of an even limb 2q+2 also carries the overflow of pair q
+// (limb 0: minus the last pair's).  m0's parity depends on y only (workgroup-uniform).
+template <int PP>
+__device__ __forceinline__ Pr rp_get_gen(const RX<PP> &X, int j, int pp, u64 e, u64 N)
+{
+    constexpr int l = RX<PP>::l;
+    const bool sg = e >= N;
+    if (sg) e -= N;
+    const int y = (int)(e >> 5), sb = (int)(e & 31);
+    const int u0 = 4 * pp - y - 1;     // >= -2l
+    const int m0 = u0 >> 1, odd = u0 & 1;
+    const u64 *F = X.f(j);
+    const short *H = X.h(j);
+    i64 seq[6];
+    bool swr[3];   // wrap flag per limb: applies to each part *after* the sub-digit split (as bp_ld)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        int m = m0 + k;
+        const bool wr = m < 0;
+        m += wr ? l : 0;
+        const u64 f = F[m];
+        i64 lo = (i64)(u32)f;
+        if (!((m0 + k) & 1)) {         // uniform: even limb, takes a pair overflow
+            const i64 hv = H[m ? (m >> 1) - 1 : l / 2 - 1];
+            lo += m ? hv : -hv;
+        }
+        seq[2 * k] = lo;
+        seq[2 * k + 1] = (i64)(f >> 32);
+        swr[k] = wr;
+    }
+    i64 o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        // source digits D[k+1], D[k] = seq[odd + k + 1], seq[odd + k] (selects: odd is uniform,
+        // and a runtime index would put seq in scratch)
+        const i64 d1 = odd ? seq[k + 2] : seq[k + 1], d0 = odd ? seq[k + 1] : seq[k];
+        const bool w1 = odd ? swr[(k + 2) >> 1] : swr[(k + 1) >> 1], w0 = odd ? swr[(k + 1) >> 1] : swr[k >> 1];
+        o[k] = bp_cneg(bp_lo(d1, sb), w1) + bp_cneg(bp_hi(d0, sb), w0);
+    }
+    if (sg) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = -o[k];
+    }
+    const i128 t0 = (i128)o[0] + ((i128)o[1] << 32);
+    const i128 t1 = (i128)o[2] + ((i128)o[3] << 32) + (t0 >> 64);
+    Pr r;
+    r.a = (u64)t0;
+    r.b = (u64)t1;
+    r.h = (int)(i64)(t1 >> 64);
+    return r;
+}
+
+// DIF pending exponent of slot s after `done` levels (bp_pend without the MFA twiddle
+// term: rp applies that on load)
+template <int LOGG>
+__device__ __forceinline__ u64 rp_pend(const PassArgs &a, const BGeo &g, int done, int s, u64 N2)
+{
+    u64 e = 0;
+    for (int j = 0; j < done; ++j)
+        if ((s >> (LOGG - 1 - j)) & 1) {
+            const int x = s & ~(((1 << (done - 1 - j)) - 1) << (LOGG - done));
+            e = bp_mod2n(e + bp_tw<LOGG, 0>(a, g, j, x), N2);
+        }
+    return e;
+}
+
+// x_i <- 2^E(i) x_i for all G slots (general exponents), NX slots per LDS round
+template <int G, int PP, int NX, typename EF>
+__device__ __forceinline__ void rp_rot_all(Pr (&x)[G][PP], const RX<PP> &X, EF efn, u64 N, int t)
+{
+#pragma unroll
+    for (int i0 = 0; i0 < G; i0 += NX) {
+#pragma unroll
+        for (int q = 0; q < NX && i0 + q < G; ++q) rp_pub<PP>(X, q, x[i0 + q], t);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < NX && i0 + q < G; ++q) {
+            const u64 e = efn(i0 + q);
+            if (e == 0) continue;   // workgroup-uniform
+#pragma unroll
+            for (int r = 0; r < PP; ++r) {
+                RP_FENCE();   // one pair position at a time (VGPRs)
+                x[i0 + q][r] = rp_get_gen<PP>(X, q, t + RP_NT * r, e, N);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// MODE: DIR 0: 0 plain, 1 MFA twiddle on load, 2 split on load (first column pass);
+//       DIR 1: 0 plain, 1 general final multipliers (inverse twiddle / scaling)
+template <int LOGG, int PP, int DIR, int MODE>
+__global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
+{
+    constexpr bool GX = MODE == 1, SPLIT = DIR == 0 && MODE == 2;
+    pass_clear_flags(a);
+    constexpr int G = 1 << LOGG, NX = G / 2 > 2 ? G / 2 : 2;
+    constexpr int l = 1024 * PP, HP = l / 2, cbw = 2 * l / 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const RX<PP> X{smem};
+    const int t = threadIdx.x;
+    const u64 N = a.N, N2 = 2 * a.N;
+    const int op = blockIdx.y;
+    Coef st;
+    st.dig = a.dig[op];
+    st.cb = a.cb[op];
+    st.top = a.top[op];
+    // group geometry is workgroup-uniform: keep it in SGPRs (readfirstlane), the VGPRs
+    // are all needed for the coefficients
+    const int sub = __builtin_amdgcn_readfirstlane((int)(blockIdx.x / a.ngroups));
+    const int grp = __builtin_amdgcn_readfirstlane((int)(blockIdx.x % a.ngroups));
+    const int lobits = a.lbM - a.lvl0 - LOGG;
+    const int lo = grp & ((1 << lobits) - 1);
+    const int hi = grp >> lobits;
+    const int bstart = hi << (a.lbM - a.lvl0);
+    if (DIR == 0 && bstart >= a.need) return;   // whole block past the truncation point (workgroup-uniform)
+    BGeo g;
+    g.pos0 = bstart | lo;
+    g.pstep = 1 << lobits;
+    g.sbase = (long)sub * a.sub_stride;
+    const u64 rsub = a.tw_mode ? (u64)revbin_dev(a.sub_off + sub, a.tw_lbR) : 0;
+    g.tw0 = a.tw_w * (u64)(a.pos_off + g.pos0) * rsub;
+    g.twst = a.tw_w * (u64)g.pstep * rsub;
+    auto slot_lane = [&](int i) -> long {   // any i (the code staging has two slots per wave)
+        const int ps = a.pos_off + g.pos0 + i * g.pstep;
+        return g.sbase + (long)(ps >> a.pbb) * a.pbs + (long)(ps & ((1 << a.pbb) - 1)) * a.pos_stride;
+    };
+    auto slot_of = [&](int i) -> long { return wv_uniform(slot_lane(i)); };   // i wave-uniform: SGPRs
+    // zero inputs (positions >= zero_from) only occur in the split pass (host: rp_usable)
+    auto zero_in = [&](int i) -> bool { return SPLIT && g.pos0 + i * g.pstep >= a.zero_from; };
+    const u64 *src = SPLIT ? a.src[op] : nullptr;
+
+    // ---- load ------------------------------------------------------------------------
+    // carry masks -> one 16-bit code per limb pair in LDS (low byte: carry out of limb 2pp,
+    // high byte: carry out of limb 2pp+1, plus the carry limb for the last pair); one
+    // thread per (slot, 64-limb row), the exchange slots are free until the levels
+    unsigned short *CODE = (unsigned short *)smem;   // G HP codes
+    if (!SPLIT) {
+        constexpr int rows = l / 64;
+        if (t < G * rows) {
+            const int i = t / rows, W = t % rows;
+            const long sl = slot_lane(i);
+            const rp_v2u pn = *(const rp_v2u *)(st.cb + (size_t)sl * cbw + 2 * W);
+            const int tv = W == rows - 1 ? st.top[sl] : 0;
+            rp_v2u *dst = (rp_v2u *)(CODE + i * HP + 32 * W);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {   // 8 codes = 16 bytes per store
+                u64 w[2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    u64 acc = 0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int j = 8 * c + 4 * h + k, b = 2 * j;   // pair 32 W + j: limbs b, b+1 of the row
+                        const int c0 = (int)((pn.x >> b) & 1) - (int)((pn.y >> b) & 1);
+                        int c1 = (int)((pn.x >> (b + 1)) & 1) - (int)((pn.y >> (b + 1)) & 1);
+                        c1 += j == 31 ? tv : 0;
+                        acc |= (u64)((c0 & 0xff) | ((c1 & 0xff) << 8)) << (16 * k);
+                    }
+                    w[h] = acc;
+                }
+                dst[c] = rp_v2u{w[0], w[1]};
+            }
+        }
+    }
+    Pr x[G][PP];
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+        if (SPLIT) __builtin_amdgcn_sched_barrier(0);   // split: 3 source limbs per pair, a slot at a time
+        const bool z = zero_in(i);
+        const long sl = z ? 0 : slot_of(i);
+#pragma unroll
+        for (int r = 0; r < PP; ++r) {
+            const int pp = t + RP_NT * r;
+            x[i][r] = Pr{0, 0, 0};
+            if (z) continue;
+            if (SPLIT) {   // first forward column pass: FFT_split_bits fused into the load
+                const u64 left = (u64)pp * 128 < a.bits1 ? a.bits1 - (u64)pp * 128 : 0;   // bits of the coefficient here
+                const long j = (long)(a.pos_off + g.pos0 + i * g.pstep) * a.jNC + a.sub_off + sub;
+                const u64 off = (u64)j * a.bits1 + (u64)pp * 128;
+                const long q = (long)(off >> 6);
+                const int sh = (int)(off & 63);
+                const long ns = left ? a.nsrc[op] : 0;
+                const u64 x0 = q < ns ? src[q] : 0, x1 = q + 1 < ns ? src[q + 1] : 0, x2 = q + 2 < ns ? src[q + 2] : 0;
+                u64 f0 = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
+                u64 f1 = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
+                f0 = left < 64 ? f0 & ((((u64)1) << left) - 1) : f0;
+                f1 = left <= 64 ? 0 : left < 128 ? f1 & ((((u64)1) << (left - 64)) - 1) : f1;
+                x[i][r].a = f0;
+                x[i][r].b = f1;
+            } else {
+                const rp_v2u v = *(const rp_v2u *)(st.dig + (size_t)sl * l + 2 * pp);
+                x[i][r].a = v.x;
+                x[i][r].b = v.y;
+            }
+        }
+    }
+    __syncthreads();
+    if (!SPLIT) {   // limb 2pp's carry c0 moves into limb 2pp+1; limb 2pp+1's (and the carry limb) is h
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+#pragma unroll
+            for (int r = 0; r < PP; ++r) {
+                RP_FENCE();   // one code read at a time (else all are hoisted: VGPRs)
+                const int pp = t + RP_NT * r;
+                const int code = CODE[i * HP + pp];
+                const int c0 = (signed char)(code & 0xff), c1 = (signed char)(code >> 8);
+                // branch-free (divergent branches here cost the allocator dearly): b += c0
+                const u64 ob = x[i][r].b, nb = ob + (u64)(i64)c0;
+                const int cc = c0 > 0 ? (int)(nb < ob) : -(int)(nb > ob);
+                x[i][r].b = nb;
+                x[i][r].h = c1 + cc;
+            }
+        }
+        __syncthreads();   // CODE aliases the exchange slots the levels publish into
+    }
+    if (DIR == 0 && GX) {   // MFA twiddle 2^(tw0 + s twst) of slot s (README:89), so every level is pair-aligned
+        rp_rot_all<G, PP, NX>(x, X, [&](int s) -> u64 { return bp_mod2n(g.tw0 + (u64)s * g.twst, N2); }, N, t);
+    }
+
+    // ---- levels ----------------------------------------------------------------------
+#pragma unroll
+    for (int li = 0; li < LOGG; ++li) {
+        const int JB = DIR == 0 ? LOGG - 1 - li : li;
+        const bool full = li == LOGG - 1;
+        if (DIR == 0 && full) {
+            // out_i = 2^Pi x_i + 2^Pk x_k,  out_k = 2^(Pi+t) x_i - 2^(Pk+t) x_k  (pairs (2q, 2q+1))
+            constexpr int QR = NX / 2;   // pairs per LDS round
+#pragma unroll
+            for (int q0 = 0; q0 < G / 2; q0 += QR) {
+#pragma unroll
+                for (int q = 0; q < QR; ++q) {
+                    rp_pub<PP>(X, 2 * q, x[2 * (q0 + q)], t);
+                    rp_pub<PP>(X, 2 * q + 1, x[2 * (q0 + q) + 1], t);
+                }
+                __syncthreads();
+#pragma unroll
+                for (int q = 0; q < QR; ++q) {
+                    const int i = 2 * (q0 + q), k = i + 1;
+                    RP_DBG_SYNC();
+                    const u64 Pi = rp_pend<LOGG>(a, g, li, i, N2), Pk = rp_pend<LOGG>(a, g, li, k, N2);
+                    const u64 tw = bp_tw<LOGG, 0>(a, g, li, k);
+                    const u64 ak = bp_mod2n(Pi + tw, N2), bk = bp_mod2n(Pk + tw, N2);
+#pragma unroll
+                    for (int r = 0; r < PP; ++r) {
+                        RP_FENCE();   // one pair position at a time (VGPRs)
+                        const int pp = t + RP_NT * r;
+                        bool n0, n1;
+                        {
+                            const Pr xi = rp_get_al<PP>(X, 2 * q, pp, Pi, N, n0);
+                            const Pr xk = rp_get_al<PP>(X, 2 * q + 1, pp, Pk, N, n1);
+                            x[i][r] = pr_add(pr_cneg(xi, n0), pr_cneg(xk, n1));
+                        }
+                        RP_FENCE();   // out_i before the reads of out_k (VGPRs)
+                        {
+                            const Pr yi = rp_get_al<PP>(X, 2 * q, pp, ak, N, n0);
+                            const Pr yk = rp_get_al<PP>(X, 2 * q + 1, pp, bk, N, n1);
+                            x[k][r] = pr_sub(pr_cneg(yi, n0), pr_cneg(yk, n1));
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+            continue;
+        }
+        // partner x_k read rotated by E: (x_i, x_k) <- (x_i + 2^E x_k, x_i - 2^E x_k)
+#pragma unroll
+        for (int pi = 0; pi < G / 2; ++pi) {
+            const int i = ((pi >> JB) << (JB + 1)) | (pi & ((1 << JB) - 1));
+            rp_pub<PP>(X, pi, x[i | (1 << JB)], t);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int pi = 0; pi < G / 2; ++pi) {
+            RP_DBG_SYNC();
+            const int i = ((pi >> JB) << (JB + 1)) | (pi & ((1 << JB) - 1));
+            const int k = i | (1 << JB);
+            u64 E;
+            if (DIR == 0) {
+                const u64 Pi = rp_pend<LOGG>(a, g, li, i, N2), Pk = rp_pend<LOGG>(a, g, li, k, N2);
+                E = Pk >= Pi ? Pk - Pi : Pk + N2 - Pi;
+            } else {
+                const u64 tw = bp_mod2n(bp_tw<LOGG, 1>(a, g, li, k), N2);
+                E = tw ? N2 - tw : 0;
+            }
+#pragma unroll
+            for (int r = 0; r < PP; ++r) {
+                if (r % 2 == 0) RP_FENCE();   // two partner reads in flight at a time
+                bool ng;
+                const Pr y = rp_get_al<PP>(X, pi, t + RP_NT * r, E, N, ng);
+                pr_bfly(x[i][r], x[k][r], x[i][r], y, ng);
+            }
+        }
+        __syncthreads();
+    }
+    if (DIR == 1 && GX) {   // inverse MFA twiddle and/or fused scaling (bp_post)
+        rp_rot_all<G, PP, NX>(x, X, [&](int s) -> u64 { return bp_post(a, g, s, N2); }, N, t);
+    }
+
+    // ---- store (reduced form) --------------------------------------------------------
+    // pair overflows -> LDS, then limb 2pp takes the overflow of pair pp - 1 (pair 0: minus
+    // the last pair's, 2^N == -1); its carry out goes into the masks, limb 2pp+1 carries 0
+    short *HX = (short *)smem;   // G HP overflows (the exchange slots are free now)
+#pragma unroll
+    for (int i = 0; i < G; ++i)
+#pragma unroll
+        for (int r = 0; r < PP; ++r) HX[i * HP + t + RP_NT * r] = (short)x[i][r].h;
+    __syncthreads();
+    const int lane = t & 63, wv = t >> 6;
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+        RP_DBG_SYNC();
+        const bool keep = DIR == 1 || ((g.pos0 + i * g.pstep) & ~(g.pstep - 1)) < a.need;
+        if (!keep) continue;   // workgroup-uniform
+        const long sl = wv_uniform(slot_of(i));
+        u64 *dst = st.dig + (size_t)sl * l;
+        u64 *cbp = st.cb + (size_t)sl * cbw;
+#pragma unroll
+        for (int r = 0; r < PP; ++r) {
+            RP_FENCE();
+            const int pp = t + RP_NT * r;
+            const int hv = HX[i * HP + (pp ? pp - 1 : HP - 1)];
+            const int hin = pp ? hv : -hv;
+            const u64 f = x[i][r].a;
+            const u64 n0 = f + (u64)(i64)hin;
+            const int k0 = hin >= 0 ? (int)(n0 < f) : -(int)(n0 > f);
+            *(rp_v2u *)(dst + 2 * pp) = rp_v2u{n0, x[i][r].b};
+            const u64 pm = __ballot(k0 == 1), nm = __ballot(k0 == -1);
+            if (lane < 2) {   // rows 2 (wv + 8r) (lanes 0..31) and +1: even-limb bits only
+                const int sh = 32 * lane;
+                const u64 pw = bp_spread((u32)(pm >> sh)), nw = bp_spread((u32)(nm >> sh));
+                *(rp_v2u *)(cbp + 2 * (2 * (wv + 8 * r) + lane)) = rp_v2u{pw, nw};
+            }
+        }
+        if (t == 0) st.top[sl] = 0;
+    }
+}

@@ -1,0 +1,33 @@
+// rpass_p1.hip -- k_rpass instantiations for l = 1024 limbs (rkernels.hpp)
+#include "rkernels.hpp"
+
+rp_fn rp_get_p1(int logg, int dir, int mode)
+{
+    static const rp_fn tab[2][3][4] = {
+        {
+            {nullptr, k_rpass<1, 1, 0, 0>, k_rpass<2, 1, 0, 0>, k_rpass<3, 1, 0, 0>},
+            {nullptr, k_rpass<1, 1, 0, 1>, k_rpass<2, 1, 0, 1>, k_rpass<3, 1, 0, 1>},
+            {nullptr, k_rpass<1, 1, 0, 2>, k_rpass<2, 1, 0, 2>, k_rpass<3, 1, 0, 2>},
+        },
+        {
+            {nullptr, k_rpass<1, 1, 1, 0>, k_rpass<2, 1, 1, 0>, k_rpass<3, 1, 1, 0>},
+            {nullptr, k_rpass<1, 1, 1, 1>, k_rpass<2, 1, 1, 1>, k_rpass<3, 1, 1, 1>},
+            {nullptr, nullptr, nullptr, nullptr},
+        },
+    };
+    if (logg < 1 || logg > 3 || dir < 0 || dir > 1 || mode < 0 || mode > 2) return nullptr;
+    return tab[dir][mode][logg];
+}
+
+rp_fn rp_get_p2(int logg, int dir, int mode);
+rp_fn rp_get_p4(int logg, int dir, int mode);
+
+rp_fn rp_get(int l, int logg, int dir, int mode)
+{
+    switch (l) {
+    case 1024: return rp_get_p1(logg, dir, mode);
+    case 2048: return rp_get_p2(logg, dir, mode);
+    case 4096: return rp_get_p4(logg, dir, mode);
+    }
+    return nullptr;
+}

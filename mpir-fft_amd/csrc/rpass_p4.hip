@@ -1,0 +1,20 @@
+// rpass_p4.hip -- k_rpass instantiations for l = 4096 limbs (rkernels.hpp)
+#include "rkernels.hpp"
+
+rp_fn rp_get_p4(int logg, int dir, int mode)
+{
+    static const rp_fn tab[2][3][3] = {
+        {
+            {nullptr, k_rpass<1, 4, 0, 0>, k_rpass<2, 4, 0, 0>},
+            {nullptr, k_rpass<1, 4, 0, 1>, k_rpass<2, 4, 0, 1>},
+            {nullptr, k_rpass<1, 4, 0, 2>, k_rpass<2, 4, 0, 2>},
+        },
+        {
+            {nullptr, k_rpass<1, 4, 1, 0>, k_rpass<2, 4, 1, 0>},
+            {nullptr, k_rpass<1, 4, 1, 1>, k_rpass<2, 4, 1, 1>},
+            {nullptr, nullptr, nullptr},
+        },
+    };
+    if (logg < 1 || logg > 2 || dir < 0 || dir > 1 || mode < 0 || mode > 2) return nullptr;
+    return tab[dir][mode][logg];
+}

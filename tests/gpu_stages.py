@@ -63,7 +63,22 @@ def _canonical(dig, top, s):
     return t == 0 or (t == 1 and not dig[s].any())
 
 
-def run_stages(mp, depth, w, a, b, dev="cuda:0", check=("fwd", "pw", "inv", "comb")):
+def _convolution(ca, cb, N, T, mul=None):
+    """c_j = sum_i ca_i cb_(j-i) for j < T (each c_j < 2^(N+1)): one Kronecker product with
+    (N + 64)-bit slots; `mul` multiplies limb arrays (GMP mpn_mul via the oracle) when given."""
+    S = N + 64
+    def pack(c):
+        return b"".join(v.to_bytes(S // 8, "little") for v in c)
+    if mul is None:
+        C = int.from_bytes(pack(ca), "little") * int.from_bytes(pack(cb), "little")
+    else:
+        r = mul(np.frombuffer(pack(ca), dtype=np.uint64), np.frombuffer(pack(cb), dtype=np.uint64))
+        C = int.from_bytes(np.ascontiguousarray(r).tobytes(), "little")
+    mask = (1 << S) - 1
+    return [(C >> (j * S)) & mask for j in range(T)]
+
+
+def run_stages(mp, depth, w, a, b, dev="cuda:0", check=("fwd", "pw", "inv", "comb"), mul=None):
     """Returns a list of failure strings (empty = all stages exact)."""
     import torch
     n1, n2 = len(a), len(b)
@@ -84,7 +99,13 @@ def run_stages(mp, depth, w, a, b, dev="cuda:0", check=("fwd", "pw", "inv", "com
     fails = []
 
     def X(x, k):
-        return sum(xj * pow(2, (w * j * k) % (2 * N), p) for j, xj in enumerate(x) if xj) % p
+        # sum_j x_j 2^(w j k) mod p, with 2^e == -2^(e - N) for N <= e < 2N (shifts, no modexp)
+        acc = 0
+        for j, xj in enumerate(x):
+            if xj:
+                e = (w * j * k) % (2 * N)
+                acc += xj << e if e < N else -(xj << (e - N))
+        return acc % p
 
     mp.stage(mp.STAGE_FWD_COLUMNS, da, db, dr, n1, n2, depth, w, ws)
     mp.stage(mp.STAGE_FWD_ROWS, da, db, dr, n1, n2, depth, w, ws)
@@ -123,8 +144,9 @@ def run_stages(mp, depth, w, a, b, dev="cuda:0", check=("fwd", "pw", "inv", "com
         dig, top = _slots(mp, ws, n1, n2, depth, w, 0)
         ca = chunks(A, P["j1"], bits1)
         cb = chunks(B, P["j2"], bits1)
+        cw = _convolution(ca, cb, N, T, mul)
         for j in range(T):
-            want = sum(ca[i] * cb[j - i] for i in range(max(0, j - len(cb) + 1), min(j, len(ca) - 1) + 1))
+            want = cw[j]
             got = _val(dig, top, j, N)
             if got != want:
                 fails.append(f"inverse coeff {j}: got {got:x} (top {top[j]}) want {want:x}")

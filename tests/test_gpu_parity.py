@@ -33,16 +33,21 @@ STAGE_SHAPES = [(6, 1, 3, 2), (6, 1, 1, 1), (7, 1, 5, 4), (7, 3, 13, 2), (8, 2, 
 # coefficient sizes l = 128 ... 4096 limbs: the int8-MFMA pointwise (k_pwm, k_pwm2)
 MFMA_SHAPES = [(9, 16, 2000, 1500), (8, 64, 3000, 2000), (7, 256, 4000, 3000), (6, 1024, 6000, 5000),
                (5, 4096, 8000, 8000), (6, 4096, 20000, 20000)]
+# l = 2048 / 4096 with enough levels for the register-resident passes (k_rpass): 3-level
+# column / row passes, the twiddle-on-load first row pass, the general-multiplier last
+# inverse row pass, the fused split; truncation case a (T <= n) and b (T > n)
+BIG_SHAPES = [(8, 512, 40000, 40000), (8, 512, 140000, 140000), (8, 512, 100000, 30000),
+              (7, 2048, 150000, 120000), (9, 256, 120000, 200000)]
 
 
-@pytest.mark.parametrize("depth,w,n1,n2", STAGE_SHAPES + MFMA_SHAPES)
-def test_stages_exact(mp, torch_dev, depth, w, n1, n2):
+@pytest.mark.parametrize("depth,w,n1,n2", STAGE_SHAPES + MFMA_SHAPES + BIG_SHAPES)
+def test_stages_exact(mp, oracle, torch_dev, depth, w, n1, n2):
     from gpu_stages import run_stages
     if not valid_shape(depth, w, n1, n2):
         pytest.skip("shape does not fit")
     a = mp.fill_random(n1, 1000 + depth * 7 + n1)
     b = mp.fill_random(n2, 2000 + w * 3 + n2)
-    fails = run_stages(mp, depth, w, a, b, dev=torch_dev)
+    fails = run_stages(mp, depth, w, a, b, dev=torch_dev, mul=oracle.gmp_mul)
     assert not fails, "\n".join(fails[:5])
 
 
