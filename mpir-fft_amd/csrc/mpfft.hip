@@ -320,6 +320,8 @@ struct Exec {
             allow_lds((const void *)f, lds);
             a.ngroups = 1 << (a.lbM - logg);
             dim3 grid((unsigned)((long)a.nsub * a.ngroups), (unsigned)nops);
+            static const bool stamps = getenv("MPFFT_RP_STAMPS") != nullptr;
+            if (stamps) return bp_stamped(f, grid, RP_NT, lds, a, logg, dir);
             hipLaunchKernelGGL(f, grid, dim3(RP_NT), lds, s, a);
             HIPCHK(hipGetLastError());
             return MPFFT_OK;
@@ -408,7 +410,7 @@ struct Exec {
             for (int k = 1; k < 8; ++k)
                 if (q[k]) { sum[k] += (double)(q[k] - prev); prev = q[k]; }
         }
-        fprintf(stderr, "bp_stamps logg=%d dir=%d l=%ld groups=%ld/%zu span=%llu ticks: load %.0f lv0 %.0f lv1 %.0f lv2 %.0f lv3 %.0f canon %.0f store %.0f\n",
+        fprintf(stderr, "%s logg=%d dir=%d l=%ld groups=%ld/%zu span=%llu ticks: load %.0f lv0 %.0f lv1 %.0f lv2 %.0f fin %.0f canon/hx %.0f store %.0f\n", nthr == RP_NT ? "rp_stamps" : "bp_stamps",
                 logg, dir, P.l, cnt, nwg, t1 - t0, sum[1] / cnt, sum[2] / cnt, sum[3] / cnt, sum[4] / cnt, sum[5] / cnt,
                 sum[6] / cnt, sum[7] / cnt);
         free(h);

@@ -16,10 +16,10 @@ rp_fn rp_get(int l, int logg, int dir, int mode);
 // most levels per pass: G l <= 16384 limbs per workgroup (32 limbs per thread)
 inline int rp_maxlogg(int l) { return l == 1024 ? 3 : l == 2048 ? 3 : l == 4096 ? 2 : 0; }   // l = 1024: G = 16 spills
 
-// LDS: NX exchange slots of 9 l bytes (limbs + 16-bit pair overflows).  <= 73 728 B,
-// so two workgroups fit in 160 KiB.
+// LDS: NX exchange slots of 9 l bytes (limbs + 16-bit pair overflows) and the exponent
+// table.  <= 73 984 B, so two workgroups fit in 160 KiB.
 inline size_t rp_lds(int l, int logg)
 {
     const int G = 1 << logg, NX = G / 2 > 2 ? G / 2 : 2;
-    return (size_t)NX * 9 * l;
+    return (size_t)NX * 9 * l + 4 * (size_t)(3 * G + (G / 2) * logg);   // + exponent and slot tables
 }

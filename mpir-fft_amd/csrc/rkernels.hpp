@@ -34,58 +34,76 @@
 
 typedef unsigned long long rp_v2u __attribute__((ext_vector_type(2)));
 
-// compiler-only memory barrier: keeps LDS reads from being hoisted en masse (each hoisted
-// read holds its VGPRs; the coefficients already take 80 of the 128)
-#define RP_FENCE() asm volatile("" ::: "memory")
-// diagnostics only (MPFFT_ABLATE & 1): a workgroup barrier wherever a phase could race
-#define RP_DBG_SYNC() do { if (a.ablate & 1) __syncthreads(); } while (0)
+// compiler-only barrier (IR memory order + machine scheduling): keeps LDS reads and the
+// arithmetic on them from being hoisted or interleaved en masse (each hoisted value holds
+// VGPRs or a 64-bit carry mask in SGPRs; the coefficients already take 80 of the 128 VGPRs)
+#define RP_FENCE() do { asm volatile("" ::: "memory"); __builtin_amdgcn_sched_barrier(0); } while (0)
+
+typedef unsigned int rp_v4u __attribute__((ext_vector_type(4)));
 
 struct Pr {
-    u64 a, b;   // limbs 2q, 2q+1
+    u32 w[4];   // limbs 2q, 2q+1 as 32-bit words (no 64-bit register-pair constraints)
     int h;      // overflow: weight 2^128 (into limb 2q+2; the last pair's weighs 2^N == -1)
 };
 
-__device__ __forceinline__ Pr pr_add(const Pr &x, const Pr &y)
+__device__ __forceinline__ Pr pr_make(rp_v4u v, int h)
 {
     Pr r;
-    u64 t;
-    const bool c0 = __builtin_add_overflow(x.a, y.a, &r.a);
-    const bool c1 = __builtin_add_overflow(x.b, y.b, &t);
-    const bool c2 = __builtin_add_overflow(t, (u64)c0, &r.b);
-    r.h = x.h + y.h + (int)c1 + (int)c2;
+    r.w[0] = v.x;
+    r.w[1] = v.y;
+    r.w[2] = v.z;
+    r.w[3] = v.w;
+    r.h = h;
+    return r;
+}
+__device__ __forceinline__ rp_v4u pr_words(const Pr &x) { return rp_v4u{x.w[0], x.w[1], x.w[2], x.w[3]}; }
+
+// 128-bit + overflow arithmetic as 32-bit add/sub-with-carry chains (v_add_co/v_addc:
+// five VALU ops per add; the overflow builtins on u64 cost compares and selects instead)
+__device__ __forceinline__ u32 lo32(u64 v) { return (u32)v; }
+__device__ __forceinline__ u32 hi32(u64 v) { return (u32)(v >> 32); }
+__device__ __forceinline__ u64 mk64(u32 lo, u32 hi) { return ((u64)hi << 32) | lo; }
+
+// x + (y ^ m) + cin  (m = 0 or ~0: with cin = 1 that is x - y)
+__device__ __forceinline__ Pr pr_addx(const Pr &x, const Pr &y, u32 m, u32 cin)
+{
+    u32 c;
+    Pr r;
+    r.w[0] = __builtin_addc(x.w[0], y.w[0] ^ m, cin, &c);
+    r.w[1] = __builtin_addc(x.w[1], y.w[1] ^ m, c, &c);
+    r.w[2] = __builtin_addc(x.w[2], y.w[2] ^ m, c, &c);
+    r.w[3] = __builtin_addc(x.w[3], y.w[3] ^ m, c, &c);
+    r.h = (int)__builtin_addc((u32)x.h, (u32)y.h ^ m, c, &c);
     return r;
 }
 
-__device__ __forceinline__ Pr pr_sub(const Pr &x, const Pr &y)
-{
-    Pr r;
-    u64 t;
-    const bool b0 = __builtin_sub_overflow(x.a, y.a, &r.a);
-    const bool b1 = __builtin_sub_overflow(x.b, y.b, &t);
-    const bool b2 = __builtin_sub_overflow(t, (u64)b0, &r.b);
-    r.h = x.h - y.h - (int)b1 - (int)b2;
-    return r;
-}
+__device__ __forceinline__ Pr pr_add(const Pr &x, const Pr &y) { return pr_addx(x, y, 0u, 0u); }
+__device__ __forceinline__ Pr pr_sub(const Pr &x, const Pr &y) { return pr_addx(x, y, ~0u, 1u); }
 
-// x +- y with the sign of y folded in: (x + s y, x - s y), s = -1 when neg
+// (x + s y, x - s y), s = -1 when neg: x + (y ^ m) + neg and x + (y ^ ~m) + !neg
 __device__ __forceinline__ void pr_bfly(Pr &u, Pr &v, const Pr &x, const Pr &y, bool neg)
 {
-    const Pr p = pr_add(x, y), m = pr_sub(x, y);
-    u = neg ? m : p;
-    v = neg ? p : m;
+    const u32 m = neg ? ~0u : 0u;
+    const Pr p = pr_addx(x, y, m, (u32)neg), q = pr_addx(x, y, ~m, (u32)!neg);
+    u = p;
+    v = q;
 }
 
-// branch-free (the sign varies per lane): -x = (~x + 1) in the 128 bits, h -> -h - (x != 0)
+// branch-free (the sign varies per lane): -x = ~x + 1 over the words and the overflow
 __device__ __forceinline__ Pr pr_cneg(const Pr &x, bool neg)
 {
-    const u64 m = neg ? MPF_MAXL : 0;
-    Pr r;
-    u64 t;
-    const bool c0 = __builtin_add_overflow(x.a ^ m, (u64)neg, &r.a);
-    const bool c1 = __builtin_add_overflow(x.b ^ m, (u64)c0, &t);
-    r.b = t;
-    r.h = (neg ? ~x.h : x.h) + (int)c1;
-    return r;
+    const Pr z = {{0, 0, 0, 0}, 0};
+    const u32 m = neg ? ~0u : 0u;
+    return pr_addx(z, x, m, (u32)neg);
+}
+
+// (lo, hi) += sext(d) for a small signed d, in place; cout = the carry out in {-1, 0, 1}
+__device__ __forceinline__ void add_small(u32 &lo, u32 &hi, int d, int &cout)
+{
+    u32 c;
+    lo = __builtin_addc(lo, (u32)d, 0u, &c);
+    hi = __builtin_addc(hi, d < 0 ? ~0u : 0u, c, &c);
+    cout = (int)c - (d < 0 ? 1 : 0);
 }
 
 // exchange slot j: limbs (8 l bytes) then pair overflows (l/2 int16)
@@ -104,7 +122,7 @@ __device__ __forceinline__ void rp_pub(const RX<PP> &X, int j, const Pr (&x)[PP]
 #pragma unroll
     for (int r = 0; r < PP; ++r) {
         const int pp = t + RP_NT * r;
-        *(rp_v2u *)(X.f(j) + 2 * pp) = rp_v2u{x[r].a, x[r].b};
+        *(rp_v4u *)(X.f(j) + 2 * pp) = pr_words(x[r]);
         X.h(j)[pp] = (short)x[r].h;
     }
 }
@@ -112,7 +130,7 @@ __device__ __forceinline__ void rp_pub(const RX<PP> &X, int j, const Pr (&x)[PP]
 // pair pp of 2^e y, y published in slot j; e a multiple of 128 bits (whole pairs), e < 2N.
 // Returns the pair unsigned; neg = its sign.
 template <int PP>
-__device__ __forceinline__ Pr rp_get_al(const RX<PP> &X, int j, int pp, u64 e, u64 N, bool &neg)
+__device__ __forceinline__ Pr rp_get_al(const RX<PP> &X, int j, int pp, u32 e, u32 N, bool &neg)
 {
     constexpr int HP = RX<PP>::l / 2;
     const bool sg = e >= N;
@@ -120,11 +138,7 @@ __device__ __forceinline__ Pr rp_get_al(const RX<PP> &X, int j, int pp, u64 e, u
     int src = pp - Yp;
     const bool wr = src < 0;
     src += wr ? HP : 0;
-    const rp_v2u v = *(const rp_v2u *)(X.f(j) + 2 * src);
-    Pr r;
-    r.a = v.x;
-    r.b = v.y;
-    r.h = X.h(j)[src];
+    const Pr r = pr_make(*(const rp_v4u *)(X.f(j) + 2 * src), X.h(j)[src]);
     neg = wr != sg;
     return r;
 }
@@ -134,7 +148,7 @@ __device__ __forceinline__ Pr rp_get_al(const RX<PP> &X, int j, int pp, u64 e, u
 // 2^N == -1); the low digit of an even limb 2q+2 also carries the overflow of pair q
 // (limb 0: minus the last pair's).  m0's parity depends on y only (workgroup-uniform).
 template <int PP>
-__device__ __forceinline__ Pr rp_get_gen(const RX<PP> &X, int j, int pp, u64 e, u64 N)
+__device__ __forceinline__ Pr rp_get_gen(const RX<PP> &X, int j, int pp, u32 e, u32 N)
 {
     constexpr int l = RX<PP>::l;
     const bool sg = e >= N;
@@ -177,29 +191,50 @@ __device__ __forceinline__ Pr rp_get_gen(const RX<PP> &X, int j, int pp, u64 e, 
     const i128 t0 = (i128)o[0] + ((i128)o[1] << 32);
     const i128 t1 = (i128)o[2] + ((i128)o[3] << 32) + (t0 >> 64);
     Pr r;
-    r.a = (u64)t0;
-    r.b = (u64)t1;
+    r.w[0] = (u32)t0;
+    r.w[1] = (u32)((u64)t0 >> 32);
+    r.w[2] = (u32)t1;
+    r.w[3] = (u32)((u64)t1 >> 32);
     r.h = (int)(i64)(t1 >> 64);
     return r;
+}
+
+// Exponents in 32 bits: every one is reduced mod 2N < 2^20 (l <= 4096), and a level
+// twiddle (k_pass :212-229) is below N (SGPR pressure: the 64-bit forms spilled).
+__device__ __forceinline__ u32 rp_mod2n(u32 e, u32 N2)
+{
+    e = e >= 2 * N2 ? e - 2 * N2 : e;
+    return e >= N2 ? e - N2 : e;
+}
+
+// level twiddle of the pair whose upper element is k at level index li (bp_tw in 32 bits)
+template <int LOGG, int DIR>
+__device__ __forceinline__ u32 rp_tw(const PassArgs &a, const BGeo &g, int li, int k)
+{
+    const int JB = DIR == 0 ? LOGG - 1 - li : li;
+    const int level = DIR == 0 ? a.lvl0 + li : a.lvl0 + LOGG - 1 - li;
+    const u32 h = 1u << (a.lbM - level - 1);
+    const u32 unit = (u32)a.rho << level;
+    return (u32)(g.pos0 & (h - 1)) * unit + (u32)(k & ((1 << JB) - 1)) * (u32)g.pstep * unit;
 }
 
 // DIF pending exponent of slot s after `done` levels (bp_pend without the MFA twiddle
 // term: rp applies that on load)
 template <int LOGG>
-__device__ __forceinline__ u64 rp_pend(const PassArgs &a, const BGeo &g, int done, int s, u64 N2)
+__device__ __forceinline__ u32 rp_pend(const PassArgs &a, const BGeo &g, int done, int s, u32 N2)
 {
-    u64 e = 0;
+    u32 e = 0;
     for (int j = 0; j < done; ++j)
         if ((s >> (LOGG - 1 - j)) & 1) {
             const int x = s & ~(((1 << (done - 1 - j)) - 1) << (LOGG - done));
-            e = bp_mod2n(e + bp_tw<LOGG, 0>(a, g, j, x), N2);
+            e = rp_mod2n(e + rp_tw<LOGG, 0>(a, g, j, x), N2);
         }
     return e;
 }
 
 // x_i <- 2^E(i) x_i for all G slots (general exponents), NX slots per LDS round
 template <int G, int PP, int NX, typename EF>
-__device__ __forceinline__ void rp_rot_all(Pr (&x)[G][PP], const RX<PP> &X, EF efn, u64 N, int t)
+__device__ __forceinline__ void rp_rot_all(Pr (&x)[G][PP], const RX<PP> &X, EF efn, u32 N, int t)
 {
 #pragma unroll
     for (int i0 = 0; i0 < G; i0 += NX) {
@@ -208,12 +243,68 @@ __device__ __forceinline__ void rp_rot_all(Pr (&x)[G][PP], const RX<PP> &X, EF e
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < NX && i0 + q < G; ++q) {
-            const u64 e = efn(i0 + q);
+            const u32 e = efn(i0 + q);
             if (e == 0) continue;   // workgroup-uniform
 #pragma unroll
             for (int r = 0; r < PP; ++r) {
                 RP_FENCE();   // one pair position at a time (VGPRs)
                 x[i0 + q][r] = rp_get_gen<PP>(X, q, t + RP_NT * r, e, N);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// Every exponent a pass needs, as a table one workgroup computes once in LDS (lane e
+// computes entry e): the kernel then reads them back as uniform values instead of
+// keeping dozens of scalar products live (they spilled).  Layout: [0, G) the general
+// multipliers (MFA twiddle before a DIF pass, bp_post after a DIT pass); [G, 2G) the
+// pending exponent of each slot after the last DIF level (applied by one aligned
+// rotation round); then G/2 partner exponents per level at 2G + li G/2.
+template <int LOGG, int DIR, bool GX>
+__device__ __forceinline__ u32 rp_exp_entry(const PassArgs &a, const BGeo &g, int e, u32 N2)
+{
+    constexpr int G = 1 << LOGG;
+    if (e < G) {
+        if (!GX) return 0;
+        return DIR == 0 ? (u32)bp_mod2n(g.tw0 + (u64)e * g.twst, N2) : (u32)bp_post(a, g, e, N2);
+    }
+    if (e < 2 * G) return DIR == 0 ? rp_pend<LOGG>(a, g, LOGG, e - G, N2) : 0;
+    e -= 2 * G;
+    const int li = e / (G / 2), r = e % (G / 2);
+    if (li >= LOGG) return 0;
+    const int JB = DIR == 0 ? LOGG - 1 - li : li;
+    const int i = ((r >> JB) << (JB + 1)) | (r & ((1 << JB) - 1)), k = i | (1 << JB);
+    if (DIR == 0) {
+        const u32 Pi = rp_pend<LOGG>(a, g, li, i, N2), Pk = rp_pend<LOGG>(a, g, li, k, N2);
+        return Pk >= Pi ? Pk - Pi : Pk + N2 - Pi;
+    }
+    const u32 tw = rp_mod2n(rp_tw<LOGG, 1>(a, g, li, k), N2);
+    return tw ? N2 - tw : 0;
+}
+
+__device__ __forceinline__ u32 rp_uniform(u32 v) { return (u32)__builtin_amdgcn_readfirstlane((int)v); }
+
+// x_i <- 2^E(i) x_i for all G slots, every E a whole number of limb pairs
+template <int G, int PP, int NX, typename EF>
+__device__ __forceinline__ void rp_rot_all_al(Pr (&x)[G][PP], const RX<PP> &X, EF efn, u32 N, int t)
+{
+#pragma unroll
+    for (int i0 = 0; i0 < G; i0 += NX) {
+#pragma unroll
+        for (int q = 0; q < NX && i0 + q < G; ++q)
+            if (efn(i0 + q)) rp_pub<PP>(X, q, x[i0 + q], t);   // uniform: slot 0 (e = 0) stays put
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < NX && i0 + q < G; ++q) {
+            const u32 e = efn(i0 + q);
+            if (e == 0) continue;
+#pragma unroll
+            for (int r = 0; r < PP; ++r) {
+                RP_FENCE();
+                bool ng;
+                const Pr y = rp_get_al<PP>(X, q, t + RP_NT * r, e, N, ng);
+                x[i0 + q][r] = pr_cneg(y, ng);
             }
         }
         __syncthreads();
@@ -232,7 +323,7 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const RX<PP> X{smem};
     const int t = threadIdx.x;
-    const u64 N = a.N, N2 = 2 * a.N;
+    const u32 N = (u32)a.N, N2 = 2 * (u32)a.N;
     const int op = blockIdx.y;
     Coef st;
     st.dig = a.dig[op];
@@ -261,7 +352,20 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
     auto slot_of = [&](int i) -> long { return wv_uniform(slot_lane(i)); };   // i wave-uniform: SGPRs
     // zero inputs (positions >= zero_from) only occur in the split pass (host: rp_usable)
     auto zero_in = [&](int i) -> bool { return SPLIT && g.pos0 + i * g.pstep >= a.zero_from; };
+    // exponent table (rp_exp_entry) and the G slot indices: read back as uniform values
+    // where needed (kept live from load to store, the 64-bit slot addresses spilled)
+    constexpr int NEXP = 2 * G + (G / 2) * LOGG;
+    u32 *EXPT = (u32 *)(smem + NX * RX<PP>::SB);
+    u32 *SLT = EXPT + NEXP;
+    if (t < NEXP) EXPT[t] = rp_exp_entry<LOGG, DIR, GX>(a, g, t, N2);
+    else if (t < NEXP + G) SLT[t - NEXP] = (u32)slot_lane(t - NEXP);
+    __syncthreads();
+    auto slot_of_t = [&](int i) -> long { return (long)rp_uniform(SLT[i]); };
     const u64 *src = SPLIT ? a.src[op] : nullptr;
+    // diagnostics (MPFFT_RP_STAMPS): thread 0 stamps the phase boundaries of this workgroup
+    unsigned long long *stamp = a.dbg ? a.dbg + 8 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x) : nullptr;
+#define RP_STAMP(k) do { if (stamp && t == 0) stamp[k] = __builtin_amdgcn_s_memtime(); } while (0)
+    RP_STAMP(0);
 
     // ---- load ------------------------------------------------------------------------
     // carry masks -> one 16-bit code per limb pair in LDS (low byte: carry out of limb 2pp,
@@ -301,11 +405,11 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
     for (int i = 0; i < G; ++i) {
         if (SPLIT) __builtin_amdgcn_sched_barrier(0);   // split: 3 source limbs per pair, a slot at a time
         const bool z = zero_in(i);
-        const long sl = z ? 0 : slot_of(i);
+        const long sl = z ? 0 : slot_of_t(i);
 #pragma unroll
         for (int r = 0; r < PP; ++r) {
             const int pp = t + RP_NT * r;
-            x[i][r] = Pr{0, 0, 0};
+            x[i][r] = Pr{{0, 0, 0, 0}, 0};
             if (z) continue;
             if (SPLIT) {   // first forward column pass: FFT_split_bits fused into the load
                 const u64 left = (u64)pp * 128 < a.bits1 ? a.bits1 - (u64)pp * 128 : 0;   // bits of the coefficient here
@@ -319,12 +423,9 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
                 u64 f1 = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
                 f0 = left < 64 ? f0 & ((((u64)1) << left) - 1) : f0;
                 f1 = left <= 64 ? 0 : left < 128 ? f1 & ((((u64)1) << (left - 64)) - 1) : f1;
-                x[i][r].a = f0;
-                x[i][r].b = f1;
+                x[i][r] = pr_make(rp_v4u{(u32)f0, (u32)(f0 >> 32), (u32)f1, (u32)(f1 >> 32)}, 0);
             } else {
-                const rp_v2u v = *(const rp_v2u *)(st.dig + (size_t)sl * l + 2 * pp);
-                x[i][r].a = v.x;
-                x[i][r].b = v.y;
+                x[i][r] = pr_make(*(const rp_v4u *)(st.dig + (size_t)sl * l + 2 * pp), 0);
             }
         }
     }
@@ -338,64 +439,22 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
                 const int pp = t + RP_NT * r;
                 const int code = CODE[i * HP + pp];
                 const int c0 = (signed char)(code & 0xff), c1 = (signed char)(code >> 8);
-                // branch-free (divergent branches here cost the allocator dearly): b += c0
-                const u64 ob = x[i][r].b, nb = ob + (u64)(i64)c0;
-                const int cc = c0 > 0 ? (int)(nb < ob) : -(int)(nb > ob);
-                x[i][r].b = nb;
+                int cc;   // b += c0 (branch-free: divergent branches here cost the allocator dearly)
+                add_small(x[i][r].w[2], x[i][r].w[3], c0, cc);
                 x[i][r].h = c1 + cc;
             }
         }
         __syncthreads();   // CODE aliases the exchange slots the levels publish into
     }
+    RP_STAMP(1);
     if (DIR == 0 && GX) {   // MFA twiddle 2^(tw0 + s twst) of slot s (README:89), so every level is pair-aligned
-        rp_rot_all<G, PP, NX>(x, X, [&](int s) -> u64 { return bp_mod2n(g.tw0 + (u64)s * g.twst, N2); }, N, t);
+        rp_rot_all<G, PP, NX>(x, X, [&](int s) -> u32 { return rp_uniform(EXPT[s]); }, N, t);
     }
 
     // ---- levels ----------------------------------------------------------------------
 #pragma unroll
     for (int li = 0; li < LOGG; ++li) {
         const int JB = DIR == 0 ? LOGG - 1 - li : li;
-        const bool full = li == LOGG - 1;
-        if (DIR == 0 && full) {
-            // out_i = 2^Pi x_i + 2^Pk x_k,  out_k = 2^(Pi+t) x_i - 2^(Pk+t) x_k  (pairs (2q, 2q+1))
-            constexpr int QR = NX / 2;   // pairs per LDS round
-#pragma unroll
-            for (int q0 = 0; q0 < G / 2; q0 += QR) {
-#pragma unroll
-                for (int q = 0; q < QR; ++q) {
-                    rp_pub<PP>(X, 2 * q, x[2 * (q0 + q)], t);
-                    rp_pub<PP>(X, 2 * q + 1, x[2 * (q0 + q) + 1], t);
-                }
-                __syncthreads();
-#pragma unroll
-                for (int q = 0; q < QR; ++q) {
-                    const int i = 2 * (q0 + q), k = i + 1;
-                    RP_DBG_SYNC();
-                    const u64 Pi = rp_pend<LOGG>(a, g, li, i, N2), Pk = rp_pend<LOGG>(a, g, li, k, N2);
-                    const u64 tw = bp_tw<LOGG, 0>(a, g, li, k);
-                    const u64 ak = bp_mod2n(Pi + tw, N2), bk = bp_mod2n(Pk + tw, N2);
-#pragma unroll
-                    for (int r = 0; r < PP; ++r) {
-                        RP_FENCE();   // one pair position at a time (VGPRs)
-                        const int pp = t + RP_NT * r;
-                        bool n0, n1;
-                        {
-                            const Pr xi = rp_get_al<PP>(X, 2 * q, pp, Pi, N, n0);
-                            const Pr xk = rp_get_al<PP>(X, 2 * q + 1, pp, Pk, N, n1);
-                            x[i][r] = pr_add(pr_cneg(xi, n0), pr_cneg(xk, n1));
-                        }
-                        RP_FENCE();   // out_i before the reads of out_k (VGPRs)
-                        {
-                            const Pr yi = rp_get_al<PP>(X, 2 * q, pp, ak, N, n0);
-                            const Pr yk = rp_get_al<PP>(X, 2 * q + 1, pp, bk, N, n1);
-                            x[k][r] = pr_sub(pr_cneg(yi, n0), pr_cneg(yk, n1));
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-            continue;
-        }
         // partner x_k read rotated by E: (x_i, x_k) <- (x_i + 2^E x_k, x_i - 2^E x_k)
 #pragma unroll
         for (int pi = 0; pi < G / 2; ++pi) {
@@ -405,17 +464,9 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
         __syncthreads();
 #pragma unroll
         for (int pi = 0; pi < G / 2; ++pi) {
-            RP_DBG_SYNC();
             const int i = ((pi >> JB) << (JB + 1)) | (pi & ((1 << JB) - 1));
             const int k = i | (1 << JB);
-            u64 E;
-            if (DIR == 0) {
-                const u64 Pi = rp_pend<LOGG>(a, g, li, i, N2), Pk = rp_pend<LOGG>(a, g, li, k, N2);
-                E = Pk >= Pi ? Pk - Pi : Pk + N2 - Pi;
-            } else {
-                const u64 tw = bp_mod2n(bp_tw<LOGG, 1>(a, g, li, k), N2);
-                E = tw ? N2 - tw : 0;
-            }
+            const u32 E = rp_uniform(EXPT[2 * G + (G / 2) * li + pi]);
 #pragma unroll
             for (int r = 0; r < PP; ++r) {
                 if (r % 2 == 0) RP_FENCE();   // two partner reads in flight at a time
@@ -425,10 +476,15 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
             }
         }
         __syncthreads();
+        if (li < 3) RP_STAMP(2 + li);
+    }
+    if (DIR == 0) {   // the pending exponents of the last level (whole pairs): one aligned rotation round
+        rp_rot_all_al<G, PP, NX>(x, X, [&](int s) -> u32 { return rp_uniform(EXPT[G + s]); }, N, t);
     }
     if (DIR == 1 && GX) {   // inverse MFA twiddle and/or fused scaling (bp_post)
-        rp_rot_all<G, PP, NX>(x, X, [&](int s) -> u64 { return bp_post(a, g, s, N2); }, N, t);
+        rp_rot_all<G, PP, NX>(x, X, [&](int s) -> u32 { return rp_uniform(EXPT[s]); }, N, t);
     }
+    RP_STAMP(5);
 
     // ---- store (reduced form) --------------------------------------------------------
     // pair overflows -> LDS, then limb 2pp takes the overflow of pair pp - 1 (pair 0: minus
@@ -439,13 +495,13 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
 #pragma unroll
         for (int r = 0; r < PP; ++r) HX[i * HP + t + RP_NT * r] = (short)x[i][r].h;
     __syncthreads();
+    RP_STAMP(6);
     const int lane = t & 63, wv = t >> 6;
 #pragma unroll
     for (int i = 0; i < G; ++i) {
-        RP_DBG_SYNC();
         const bool keep = DIR == 1 || ((g.pos0 + i * g.pstep) & ~(g.pstep - 1)) < a.need;
         if (!keep) continue;   // workgroup-uniform
-        const long sl = wv_uniform(slot_of(i));
+        const long sl = slot_of_t(i);
         u64 *dst = st.dig + (size_t)sl * l;
         u64 *cbp = st.cb + (size_t)sl * cbw;
 #pragma unroll
@@ -454,17 +510,24 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
             const int pp = t + RP_NT * r;
             const int hv = HX[i * HP + (pp ? pp - 1 : HP - 1)];
             const int hin = pp ? hv : -hv;
-            const u64 f = x[i][r].a;
-            const u64 n0 = f + (u64)(i64)hin;
-            const int k0 = hin >= 0 ? (int)(n0 < f) : -(int)(n0 > f);
-            *(rp_v2u *)(dst + 2 * pp) = rp_v2u{n0, x[i][r].b};
-            const u64 pm = __ballot(k0 == 1), nm = __ballot(k0 == -1);
-            if (lane < 2) {   // rows 2 (wv + 8r) (lanes 0..31) and +1: even-limb bits only
-                const int sh = 32 * lane;
-                const u64 pw = bp_spread((u32)(pm >> sh)), nw = bp_spread((u32)(nm >> sh));
-                *(rp_v2u *)(cbp + 2 * (2 * (wv + 8 * r) + lane)) = rp_v2u{pw, nw};
-            }
+            int k0;
+            add_small(x[i][r].w[0], x[i][r].w[1], hin, k0);
+            *(rp_v4u *)(dst + 2 * pp) = pr_words(x[i][r]);
+            // mask words of rows 2 (wv + 8r) (pairs of lanes 0..31) and +1 (lanes 32..63): bit 2j
+            // is pair j's even limb (odd limbs carry nothing).  Lane L fetches the carry of pair
+            // L/2 (resp. 32 + L/2), so one ballot over the even lanes is the word.
+            const int ka = __shfl(k0, lane >> 1), kb = __shfl(k0, 32 + (lane >> 1));
+            const bool ev = !(lane & 1);
+            const u64 pa = __ballot(ev && ka == 1), na = __ballot(ev && ka == -1);
+            const u64 pb = __ballot(ev && kb == 1), nb = __ballot(ev && kb == -1);
+            if (lane < 2)
+                *(rp_v2u *)(cbp + 2 * (2 * (wv + 8 * r) + lane)) = lane ? rp_v2u{pb, nb} : rp_v2u{pa, na};
         }
         if (t == 0) st.top[sl] = 0;
     }
+    if (stamp) {
+        __syncthreads();
+        RP_STAMP(7);
+    }
+#undef RP_STAMP
 }
