@@ -501,7 +501,8 @@ struct Exec {
             PassArgs a = row_args();
             a.lvl0 = lvl;
             a.tw_mode = lvl == 0 ? 1 : 0;
-            if (lvl + k == P.lbC) a.canon = 1;
+            // canonical pointwise inputs, except for k_pwss (it loads the reduced form)
+            if (lvl + k == P.lbC) a.canon = pwss_active() ? 0 : 1;
             int rc = pass(a, k, 0, nops);
             if (rc) return rc;
             lvl += k;
@@ -523,6 +524,12 @@ struct Exec {
         return 0;
     }
 
+    bool pwss_active() const
+    {
+        const int lk = pwss_lk(P.l);
+        return lk && pw_get(pw_inner_limbs(P.l, lk), lk) != nullptr;
+    }
+
     int pointwise()
     {
         const long cnt = (long)rcount * P.NC;
@@ -540,7 +547,8 @@ struct Exec {
                     HIPCHK(hipMemsetAsync(dbg, 0, (size_t)cnt * 64, s));
                 }
                 hipLaunchKernelGGL(f, dim3((unsigned)cnt), dim3(1u << lk), lds, s, row.dig[0], row.cb[0], row.top[0],
-                                   (const u64 *)row.dig[1], (const int *)row.top[1], (int)P.l, lk, dbg);
+                                   (const u64 *)row.dig[1], (const u64 *)row.cb[1], (const int *)row.top[1], (int)P.l, lk,
+                                   dbg);
                 HIPCHK(hipGetLastError());
                 if (stamps) {
                     unsigned long long *h = (unsigned long long *)malloc((size_t)cnt * 64);
@@ -903,9 +911,9 @@ int mpfft_stage_kernels(long n1, long n2, unsigned long depth, unsigned long w, 
     int rc = make_plan(&P, n1, n2, depth, w);
     if (rc) return rc;
     const char *pass = P.big ? (P.rpass ? "k_rpass" : "k_bpass") : (P.wave && P.lds) ? "k_lpass" : P.wave ? "k_wpass" : "k_pass";
-    const char *rows = P.big && P.rpass ? "k_rpass + k_bpass (canonical last pass)" : pass;
     char pw[64];
     const int lk = Exec::pwss_lk(P.l);
+    const char *rows = P.big && P.rpass && !(lk && pw_get(pw_inner_limbs(P.l, lk), lk)) ? "k_rpass + k_bpass (canonical last pass)" : pass;
     if (lk && pw_get(pw_inner_limbs(P.l, lk), lk))
         snprintf(pw, sizeof pw, "k_pwss<%d> (nested negacyclic, K=%d)", pw_inner_limbs(P.l, lk), 1 << lk);
     else if (P.l % 256 == 0 && P.l <= 4096 && pw_kind() == 0)

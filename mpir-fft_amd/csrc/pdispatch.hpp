@@ -3,7 +3,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
-typedef void (*pw_fn)(uint64_t *, uint64_t *, int *, const uint64_t *, const int *, int, int, unsigned long long *);
+typedef void (*pw_fn)(uint64_t *, uint64_t *, int *, const uint64_t *, const uint64_t *, const int *, int, int,
+                      unsigned long long *);
 
 pw_fn pw_get(int M, int lk);       // k_pwss<M, lk> (M = inner coefficient limbs, 2^lk pieces), nullptr if not built
 size_t pw_lds(int M, int K, int l);

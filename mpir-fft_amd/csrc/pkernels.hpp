@@ -2,7 +2,7 @@
 // (the nested negacyclic transform of FFT_mulmod_2expp1 /
 // fft_mulmod_2expp1, mul_fft.c:2998-3167, FFT/IFFT_radix2_negacyclic :1290, :1861).
 //
-// One workgroup computes one product a b mod p (a, b canonical, N = 64 l bits):
+// One workgroup computes one product a b mod p (a, b in the reduced HBM form, N = 64 l bits):
 //   * a, b are cut into K = 2^lk pieces of B = N/K bits (thread t owns piece t);
 //   * the negacyclic convolution of the pieces (X^K == -1 with X = 2^B, so it IS the
 //     product mod p) is computed in the inner ring R' = Z/(2^N' + 1), N' = 64 M, with
@@ -287,11 +287,54 @@ __device__ __forceinline__ void pw_transform(u64 (&L)[M], int &T, int &S, unsign
     }
 }
 
-// k_pwss<M>: A[slot] <- A[slot] * B[slot] mod 2^N + 1, one workgroup of K = 2^lk threads
-// per slot; canonical inputs (limbs + carry limb in {0, 1}), reduced-form output.
+// Piece t of a coefficient in the reduced HBM form (coeff.hpp: limbs + carry masks +
+// carry limb): limbs [t LP, t LP + LP) plus the carries into them -- the carry out of
+// limb m lands in limb m + 1, the carry into limb 0 is minus the carry out of limb l-1
+// and minus the carry limb (both weigh 2^N == -1); the carry out of the piece's top limb
+// is the next piece's.  The value v (-2 <= v < 2^(64 LP) + 2^(64 LP - 64)) is returned as
+// L + T 2^N', T in {-1, 0}: the convolution tolerates such pieces (|c_t| < K 2^(2B+1)
+// still fits the headroom N' >= 2B + lk + 2), so the pointwise inputs need no
+// canonicalisation pass.  A piece lies inside one 64-limb mask row (LP | 64).
+template <int M, int LP>
+__device__ __forceinline__ void pw_load_piece(u64 (&L)[M], int &T, const u64 *dig, const u64 *cbp, int top, int l, int t)
+{
+    const int m0 = t * LP, W = m0 >> 6, b0 = m0 & 63;
+    const u64 pw = cbp[2 * W], nw = cbp[2 * W + 1];
+    int cin;
+    if (m0) {
+        const int Wp = (m0 - 1) >> 6, bp = (m0 - 1) & 63;
+        cin = (int)((cbp[2 * Wp] >> bp) & 1) - (int)((cbp[2 * Wp + 1] >> bp) & 1);
+    } else {
+        const int Wl = (l - 1) >> 6, bl = (l - 1) & 63;
+        cin = -((int)((cbp[2 * Wl] >> bl) & 1) - (int)((cbp[2 * Wl + 1] >> bl) & 1)) - top;
+    }
+    i64 c = cin;   // signed carry into the next limb
+#pragma unroll
+    for (int j = 0; j < LP; ++j) {
+        const u64 v = dig[m0 + j];
+        const int k = j ? (int)((pw >> (b0 + j - 1)) & 1) - (int)((nw >> (b0 + j - 1)) & 1) : 0;
+        const i64 add = c + k;        // |add| <= 4
+        const u64 r = v + (u64)add;
+        c = add >= 0 ? (i64)(r < v) : -(i64)(r > v);
+        L[j] = r;
+    }
+    // the carry c out of limb LP - 1 in {-1, 0, 1}: limb LP = c, sign-extended above (one
+    // register for all the upper limbs), top -1 for a negative piece
+    const u64 up = c < 0 ? ~0ull : 0ull;
+#pragma unroll
+    for (int j = LP; j < M; ++j) L[j] = j == LP ? (c > 0 ? 1ull : up) : up;
+    T = c < 0 ? -1 : 0;
+}
+
+// limbs per piece of the instantiated k_pwss shapes: l / K (l = 1024, 2048, 4096)
 template <int M, int LK>
-__global__ __launch_bounds__(1 << LK) void k_pwss(u64 *digA, u64 *cbA, int *topA, const u64 *digB, const int *topB,
-                                                  int l, int lk_unused, unsigned long long *dbg)
+__host__ __device__ constexpr int pw_piece_limbs() { return M == 12 ? 4 : 8; }
+
+// k_pwss<M>: A[slot] <- A[slot] * B[slot] mod 2^N + 1, one workgroup of K = 2^lk threads
+// per slot; reduced-form inputs and output (HBM format of coeff.hpp).
+template <int M, int LK>
+__global__ __launch_bounds__(1 << LK) void k_pwss(u64 *digA, u64 *cbA, int *topA, const u64 *digB, const u64 *cbB,
+                                                  const int *topB, int l, int lk_unused, unsigned long long *dbg)
 {
     // diagnostics (MPFFT_PW_STAMPS): thread 0 stamps the phase boundaries of this workgroup
     unsigned long long *stamp = dbg ? dbg + 8 * (size_t)blockIdx.x : nullptr;
@@ -316,26 +359,13 @@ __global__ __launch_bounds__(1 << LK) void k_pwss(u64 *digA, u64 *cbA, int *topA
     const int cbw = cb_words(l);
     u64 *cbp = cbA + (size_t)slot * cbw;
 
-    if (ta | tb) {
-        // 2^N == -1: the product is 1, -b or -a (mul_fft.c:3250).  -v == ~v + 2 (mod p):
-        // limbs ~v with the +2 carried by the carry limb (top = -2, weighs 2^N == -1).
-        for (int m = t; m < l; m += K) {
-            const u64 v = ta && tb ? (m == 0) : ~(ta ? pb[m] : pa[m]);
-            pa[m] = v;
-        }
-        for (int w = t; w < cbw; w += K) cbp[w] = 0;
-        if (t == 0) topA[slot] = ta && tb ? 0 : -2;
-        return;
-    }
-
-    // ---- pieces and forward transforms (A, then B held in registers) -----------------
+    // ---- pieces (reduced-form inputs) and forward transforms (A, then B in registers) ---
     u64 La[M], Lb[M];
-    int Ta = 0, Tb = 0, Sa = 0, Sb = 0;   // tops, sign flags
-#pragma unroll
-    for (int j = 0; j < M; ++j) {
-        La[j] = j < LP ? pa[(size_t)t * LP + j] : 0;
-        Lb[j] = j < LP ? pb[(size_t)t * LP + j] : 0;
-    }
+    int Ta, Tb, Sa = 0, Sb = 0;   // tops, sign flags
+    constexpr int CLP = pw_piece_limbs<M, LK>();   // == LP (host: pw_inner_limbs)
+    pw_load_piece<M, CLP>(La, Ta, pa, cbp, ta, l, t);
+    pw_load_piece<M, CLP>(Lb, Tb, pb, cbB + (size_t)slot * cbw, tb, l, t);
+    __syncthreads();   // every piece read before any output limb is written (in place on A)
     unsigned Pa = (unsigned)t * TH, Pb = Pa;   // negacyclic weight theta^t (t TH < N')
     PW_STAMP(1);
     pw_transform<M, LK, 0>(La, Ta, Sa, Pa, Xw, TT, PP, TH, t);

@@ -3,7 +3,8 @@ tests/test_gpu_parity.py; runnable directly on the GPU box for diagnostics:
 `python tests/gpu_stages.py`).
 
 Stage specs:
-  forward  slot p*NC + q = X_{revbin(p) + NR revbin(q)} mod 2^N + 1, canonical,
+  forward  slot p*NC + q = X_{revbin(p) + NR revbin(q)} mod 2^N + 1 (canonical, or
+           reduced when the pointwise is k_pwss),
            X_k = sum_j x_j 2^(w j k) (a3 output spec, up to the reference's two
            revbin permutations which this build never performs), p < T/NC
   pointwise slot = XA * XB mod 2^N + 1, reduced form (limbs + carry masks) (a20)
@@ -113,6 +114,7 @@ def run_stages(mp, depth, w, a, b, dev="cuda:0", check=("fwd", "pw", "inv", "com
     XA, XB = {}, {}
     for which, x, store in ((0, xa, XA), (1, xb, XB)):
         dig, top = _slots(mp, ws, n1, n2, depth, w, which)
+        cbx = _cbs(mp, ws, n1, n2, depth, w, which)
         for pp in range(Tr):
             for q in range(NC):
                 s = pp * NC + q
@@ -120,8 +122,9 @@ def run_stages(mp, depth, w, a, b, dev="cuda:0", check=("fwd", "pw", "inv", "com
                 want = X(x, k)
                 store[s] = want
                 if "fwd" in check:
-                    got = _val(dig, top, s, N)
-                    if not _canonical(dig, top, s) or got != want:
+                    # canonical, or (k_pwss loads it) the reduced form: limbs + carries + top, mod p
+                    got = _val_reduced(dig, top, cbx, s, N) % p
+                    if got != want:
                         fails.append(f"fwd op{which} slot ({pp},{q}) k={k}: got {got:x} top {top[s]} want {want:x}")
                         if len(fails) > 8:
                             return fails
