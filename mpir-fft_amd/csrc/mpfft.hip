@@ -683,6 +683,13 @@ struct Exec {
         a.i0 = (int)i0;
         a.cnt = (int)cnt;
         a.rho = rho;
+        if (P.rpass) {   // register-resident pair steps (rkernels.hpp)
+            rp_pair_fn f = rp_pair_get((int)P.l, op);
+            if (!f) return MPFFT_EUNSUPPORTED;
+            hipLaunchKernelGGL(f, dim3((unsigned)(cnt * ccount)), dim3(RP_NT), rp_pair_lds((int)P.l), s, a);
+            HIPCHK(hipGetLastError());
+            return MPFFT_OK;
+        }
         if (P.wave) {
             void (*f)(PairArgs) = wv_fns(P.wU, P.wfull).pair;
             const size_t lds = (size_t)WPB * 16 * P.l;
@@ -924,7 +931,7 @@ int mpfft_stage_kernels(long n1, long n2, unsigned long depth, unsigned long w, 
         snprintf(pw, sizeof pw, "k_pw (VALU)");
     else
         snprintf(pw, sizeof pw, "k_pointwise (VALU)");
-    const char *pair = P.wave ? "k_wpair" : "k_pairop";
+    const char *pair = P.rpass ? "k_rpair" : P.wave ? "k_wpair" : "k_pairop";
     const char *scale = P.fuse_scale ? "(fused into the last inverse column pass)" : P.wave ? "k_wscale" : "k_scale";
     static const bool multi = [] { const char *e = getenv("MPFFT_COMBINE"); return e && !strcmp(e, "multi"); }();
     snprintf(buf, len, "%s;%s;%s;%s;%s + %s;%s;%s", pass, rows, pw, pass, pass, pair, scale,

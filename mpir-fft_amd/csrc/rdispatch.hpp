@@ -4,7 +4,9 @@
 #include <stddef.h>
 
 struct PassArgs;
+struct PairArgs;
 typedef void (*rp_fn)(PassArgs);
+typedef void (*rp_pair_fn)(PairArgs);
 
 #define RP_NT 512   // threads per workgroup; two workgroups share a CU
 
@@ -23,3 +25,7 @@ inline size_t rp_lds(int l, int logg)
     const int G = 1 << logg, NX = G / 2 > 2 ? G / 2 : 2;
     return (size_t)NX * 9 * l + 4 * (size_t)(3 * G + (G / 2) * logg);   // + exponent and slot tables
 }
+
+// k_rpair<PP, OP>: the truncated inverse's pair steps (OP_DOUBLE .. OP_IBFLY, kernels.hpp)
+rp_pair_fn rp_pair_get(int l, int op);
+inline size_t rp_pair_lds(int l) { return (size_t)9 * l + 16; }

@@ -311,6 +311,118 @@ __device__ __forceinline__ void rp_rot_all_al(Pr (&x)[G][PP], const RX<PP> &X, E
     }
 }
 
+// ---- HBM <-> register pairs (k_rpass, k_rpair) ------------------------------------
+// Carry masks -> one 16-bit code per limb pair in LDS (low byte: carry out of limb 2pp,
+// high byte: carry out of limb 2pp+1, plus the carry limb for the last pair); one thread
+// per (slot, 64-limb row) of the first NS slots, slot i's index at SL[i] (LDS).
+template <int NS, int PP>
+__device__ __forceinline__ void rp_stage_codes(unsigned short *CODE, const Coef &st, const u32 *SL, int t)
+{
+    constexpr int l = 1024 * PP, HP = l / 2, cbw = 2 * l / 64, rows = l / 64;
+    if (t >= NS * rows) return;
+    const int i = t / rows, W = t % rows;
+    const long sl = (long)SL[i];
+    const rp_v2u pn = *(const rp_v2u *)(st.cb + (size_t)sl * cbw + 2 * W);
+    const int tv = W == rows - 1 ? st.top[sl] : 0;
+    rp_v2u *dst = (rp_v2u *)(CODE + i * HP + 32 * W);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {   // 8 codes = 16 bytes per store
+        u64 w[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            u64 acc = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int j = 8 * c + 4 * h + k, b = 2 * j;   // pair 32 W + j: limbs b, b+1 of the row
+                const int c0 = (int)((pn.x >> b) & 1) - (int)((pn.y >> b) & 1);
+                int c1 = (int)((pn.x >> (b + 1)) & 1) - (int)((pn.y >> (b + 1)) & 1);
+                c1 += j == 31 ? tv : 0;
+                acc |= (u64)((c0 & 0xff) | ((c1 & 0xff) << 8)) << (16 * k);
+            }
+            w[h] = acc;
+        }
+        dst[c] = rp_v2u{w[0], w[1]};
+    }
+}
+
+// limbs of the first NS slots (slot i at the uniform index SL[i])
+template <int NS, int NSX, int PP>
+__device__ __forceinline__ void rp_load_limbs(Pr (&x)[NSX][PP], const Coef &st, const u32 *SL, int t)
+{
+    constexpr int l = 1024 * PP;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        const long sl = (long)rp_uniform(SL[i]);
+#pragma unroll
+        for (int r = 0; r < PP; ++r)
+            x[i][r] = pr_make(*(const rp_v4u *)(st.dig + (size_t)sl * l + 2 * (t + RP_NT * r)), 0);
+    }
+}
+
+// codes -> pair form: limb 2pp's carry moves into limb 2pp+1, limb 2pp+1's (and the carry
+// limb) is the pair overflow h.  Ends with a barrier: CODE aliases the exchange slots.
+template <int NS, int NSX, int PP>
+__device__ __forceinline__ void rp_decode(Pr (&x)[NSX][PP], const unsigned short *CODE, int t)
+{
+    constexpr int HP = 512 * PP;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+#pragma unroll
+        for (int r = 0; r < PP; ++r) {
+            RP_FENCE();   // one code read at a time (else all are hoisted: VGPRs)
+            const int code = CODE[i * HP + t + RP_NT * r];
+            const int c0 = (signed char)(code & 0xff), c1 = (signed char)(code >> 8);
+            int cc;   // b += c0 (branch-free: divergent branches here cost the allocator dearly)
+            add_small(x[i][r].w[2], x[i][r].w[3], c0, cc);
+            x[i][r].h = c1 + cc;
+        }
+    }
+    __syncthreads();
+}
+
+// store (reduced form) of the slots i < NS with keep(i): pair overflows -> LDS (HX, over the
+// exchange slots: callers end their last LDS phase with a barrier), then limb 2pp takes the
+// overflow of pair pp - 1 (pair 0: minus the last pair's, 2^N == -1); its carry out goes
+// into the masks, limb 2pp+1 carries 0
+template <int NS, int NSX, int PP, typename KEEP>
+__device__ __forceinline__ void rp_store(Pr (&x)[NSX][PP], const Coef &st, const u32 *SL, KEEP keep, short *HX, int t)
+{
+    constexpr int l = 1024 * PP, HP = l / 2, cbw = 2 * l / 64;
+#pragma unroll
+    for (int i = 0; i < NS; ++i)
+#pragma unroll
+        for (int r = 0; r < PP; ++r) HX[i * HP + t + RP_NT * r] = (short)x[i][r].h;
+    __syncthreads();
+    const int lane = t & 63, wv = t >> 6;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        if (!keep(i)) continue;   // workgroup-uniform
+        const long sl = (long)rp_uniform(SL[i]);
+        u64 *dst = st.dig + (size_t)sl * l;
+        u64 *cbp = st.cb + (size_t)sl * cbw;
+#pragma unroll
+        for (int r = 0; r < PP; ++r) {
+            RP_FENCE();
+            const int pp = t + RP_NT * r;
+            const int hv = HX[i * HP + (pp ? pp - 1 : HP - 1)];
+            const int hin = pp ? hv : -hv;
+            int k0;
+            add_small(x[i][r].w[0], x[i][r].w[1], hin, k0);
+            *(rp_v4u *)(dst + 2 * pp) = pr_words(x[i][r]);
+            // mask words of rows 2 (wv + 8r) (pairs of lanes 0..31) and +1 (lanes 32..63): bit 2j
+            // is pair j's even limb (odd limbs carry nothing).  Lane L fetches the carry of pair
+            // L/2 (resp. 32 + L/2), so one ballot over the even lanes is the word.
+            const int ka = __shfl(k0, lane >> 1), kb = __shfl(k0, 32 + (lane >> 1));
+            const bool ev = !(lane & 1);
+            const u64 pa = __ballot(ev && ka == 1), na = __ballot(ev && ka == -1);
+            const u64 pb = __ballot(ev && kb == 1), nb = __ballot(ev && kb == -1);
+            if (lane < 2)
+                *(rp_v2u *)(cbp + 2 * (2 * (wv + 8 * r) + lane)) = lane ? rp_v2u{pb, nb} : rp_v2u{pa, na};
+        }
+        if (t == 0) st.top[sl] = 0;
+    }
+}
+
 // MODE: DIR 0: 0 plain, 1 MFA twiddle on load, 2 split on load (first column pass);
 //       DIR 1: 0 plain, 1 general final multipliers (inverse twiddle / scaling)
 template <int LOGG, int PP, int DIR, int MODE>
@@ -368,50 +480,23 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
     RP_STAMP(0);
 
     // ---- load ------------------------------------------------------------------------
-    // carry masks -> one 16-bit code per limb pair in LDS (low byte: carry out of limb 2pp,
-    // high byte: carry out of limb 2pp+1, plus the carry limb for the last pair); one
-    // thread per (slot, 64-limb row), the exchange slots are free until the levels
-    unsigned short *CODE = (unsigned short *)smem;   // G HP codes
-    if (!SPLIT) {
-        constexpr int rows = l / 64;
-        if (t < G * rows) {
-            const int i = t / rows, W = t % rows;
-            const long sl = slot_lane(i);
-            const rp_v2u pn = *(const rp_v2u *)(st.cb + (size_t)sl * cbw + 2 * W);
-            const int tv = W == rows - 1 ? st.top[sl] : 0;
-            rp_v2u *dst = (rp_v2u *)(CODE + i * HP + 32 * W);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {   // 8 codes = 16 bytes per store
-                u64 w[2];
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    u64 acc = 0;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const int j = 8 * c + 4 * h + k, b = 2 * j;   // pair 32 W + j: limbs b, b+1 of the row
-                        const int c0 = (int)((pn.x >> b) & 1) - (int)((pn.y >> b) & 1);
-                        int c1 = (int)((pn.x >> (b + 1)) & 1) - (int)((pn.y >> (b + 1)) & 1);
-                        c1 += j == 31 ? tv : 0;
-                        acc |= (u64)((c0 & 0xff) | ((c1 & 0xff) << 8)) << (16 * k);
-                    }
-                    w[h] = acc;
-                }
-                dst[c] = rp_v2u{w[0], w[1]};
-            }
-        }
-    }
+    unsigned short *CODE = (unsigned short *)smem;   // G HP codes (over the exchange slots)
     Pr x[G][PP];
+    if (!SPLIT) {
+        rp_stage_codes<G, PP>(CODE, st, SLT, t);
+        rp_load_limbs<G, G, PP>(x, st, SLT, t);
+        __syncthreads();
+        rp_decode<G, G, PP>(x, CODE, t);
+    } else {   // first forward column pass: FFT_split_bits fused into the load
 #pragma unroll
-    for (int i = 0; i < G; ++i) {
-        if (SPLIT) __builtin_amdgcn_sched_barrier(0);   // split: 3 source limbs per pair, a slot at a time
-        const bool z = zero_in(i);
-        const long sl = z ? 0 : slot_of_t(i);
+        for (int i = 0; i < G; ++i) {
+            __builtin_amdgcn_sched_barrier(0);   // 3 source limbs per pair, a slot at a time
+            const bool z = zero_in(i);
 #pragma unroll
-        for (int r = 0; r < PP; ++r) {
-            const int pp = t + RP_NT * r;
-            x[i][r] = Pr{{0, 0, 0, 0}, 0};
-            if (z) continue;
-            if (SPLIT) {   // first forward column pass: FFT_split_bits fused into the load
+            for (int r = 0; r < PP; ++r) {
+                const int pp = t + RP_NT * r;
+                x[i][r] = Pr{{0, 0, 0, 0}, 0};
+                if (z) continue;
                 const u64 left = (u64)pp * 128 < a.bits1 ? a.bits1 - (u64)pp * 128 : 0;   // bits of the coefficient here
                 const long j = (long)(a.pos_off + g.pos0 + i * g.pstep) * a.jNC + a.sub_off + sub;
                 const u64 off = (u64)j * a.bits1 + (u64)pp * 128;
@@ -424,27 +509,8 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
                 f0 = left < 64 ? f0 & ((((u64)1) << left) - 1) : f0;
                 f1 = left <= 64 ? 0 : left < 128 ? f1 & ((((u64)1) << (left - 64)) - 1) : f1;
                 x[i][r] = pr_make(rp_v4u{(u32)f0, (u32)(f0 >> 32), (u32)f1, (u32)(f1 >> 32)}, 0);
-            } else {
-                x[i][r] = pr_make(*(const rp_v4u *)(st.dig + (size_t)sl * l + 2 * pp), 0);
             }
         }
-    }
-    __syncthreads();
-    if (!SPLIT) {   // limb 2pp's carry c0 moves into limb 2pp+1; limb 2pp+1's (and the carry limb) is h
-#pragma unroll
-        for (int i = 0; i < G; ++i) {
-#pragma unroll
-            for (int r = 0; r < PP; ++r) {
-                RP_FENCE();   // one code read at a time (else all are hoisted: VGPRs)
-                const int pp = t + RP_NT * r;
-                const int code = CODE[i * HP + pp];
-                const int c0 = (signed char)(code & 0xff), c1 = (signed char)(code >> 8);
-                int cc;   // b += c0 (branch-free: divergent branches here cost the allocator dearly)
-                add_small(x[i][r].w[2], x[i][r].w[3], c0, cc);
-                x[i][r].h = c1 + cc;
-            }
-        }
-        __syncthreads();   // CODE aliases the exchange slots the levels publish into
     }
     RP_STAMP(1);
     if (DIR == 0 && GX) {   // MFA twiddle 2^(tw0 + s twst) of slot s (README:89), so every level is pair-aligned
@@ -487,47 +553,103 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
     RP_STAMP(5);
 
     // ---- store (reduced form) --------------------------------------------------------
-    // pair overflows -> LDS, then limb 2pp takes the overflow of pair pp - 1 (pair 0: minus
-    // the last pair's, 2^N == -1); its carry out goes into the masks, limb 2pp+1 carries 0
-    short *HX = (short *)smem;   // G HP overflows (the exchange slots are free now)
-#pragma unroll
-    for (int i = 0; i < G; ++i)
-#pragma unroll
-        for (int r = 0; r < PP; ++r) HX[i * HP + t + RP_NT * r] = (short)x[i][r].h;
-    __syncthreads();
+    rp_store<G, G, PP>(x, st, SLT, [&](int i) -> bool {
+        return DIR == 1 || ((g.pos0 + i * g.pstep) & ~(g.pstep - 1)) < a.need;
+    }, (short *)smem, t);
     RP_STAMP(6);
-    const int lane = t & 63, wv = t >> 6;
-#pragma unroll
-    for (int i = 0; i < G; ++i) {
-        const bool keep = DIR == 1 || ((g.pos0 + i * g.pstep) & ~(g.pstep - 1)) < a.need;
-        if (!keep) continue;   // workgroup-uniform
-        const long sl = slot_of_t(i);
-        u64 *dst = st.dig + (size_t)sl * l;
-        u64 *cbp = st.cb + (size_t)sl * cbw;
-#pragma unroll
-        for (int r = 0; r < PP; ++r) {
-            RP_FENCE();
-            const int pp = t + RP_NT * r;
-            const int hv = HX[i * HP + (pp ? pp - 1 : HP - 1)];
-            const int hin = pp ? hv : -hv;
-            int k0;
-            add_small(x[i][r].w[0], x[i][r].w[1], hin, k0);
-            *(rp_v4u *)(dst + 2 * pp) = pr_words(x[i][r]);
-            // mask words of rows 2 (wv + 8r) (pairs of lanes 0..31) and +1 (lanes 32..63): bit 2j
-            // is pair j's even limb (odd limbs carry nothing).  Lane L fetches the carry of pair
-            // L/2 (resp. 32 + L/2), so one ballot over the even lanes is the word.
-            const int ka = __shfl(k0, lane >> 1), kb = __shfl(k0, 32 + (lane >> 1));
-            const bool ev = !(lane & 1);
-            const u64 pa = __ballot(ev && ka == 1), na = __ballot(ev && ka == -1);
-            const u64 pb = __ballot(ev && kb == 1), nb = __ballot(ev && kb == -1);
-            if (lane < 2)
-                *(rp_v2u *)(cbp + 2 * (2 * (wv + 8 * r) + lane)) = lane ? rp_v2u{pb, nb} : rp_v2u{pa, na};
-        }
-        if (t == 0) st.top[sl] = 0;
-    }
     if (stamp) {
         __syncthreads();
         RP_STAMP(7);
     }
 #undef RP_STAMP
+}
+
+// ---- element-wise steps of the truncated inverse column transform --------------------
+// k_rpair<PP, OP>: the k_pairop operations (IFFT_radix2_truncate(1)_twiddle's pair steps,
+// mul_fft.c:1604-1668, :1733-1790) on the pair (i, i + h) of one column, in the register
+// pair form: sums and differences are carry chains, the multipliers 2^e are rotations
+// through one LDS exchange slot (aligned when e is a whole number of limb pairs, else the
+// general 32-bit digit rotation; halving is 2^(2N-1)).  512 threads, 9 l bytes of LDS:
+// several workgroups per CU overlap their loads and stores.
+template <int PP, int OP>
+__global__ __launch_bounds__(RP_NT) void k_rpair(PairArgs a)
+{
+    constexpr int l = 1024 * PP;
+    constexpr bool LOADB = OP != OP_DOUBLE && OP != OP_FILL;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const RX<PP> X{smem};
+    u32 *SL = (u32 *)(smem + RX<PP>::SB);
+    const int t = threadIdx.x;
+    const int col = (int)(blockIdx.x % a.ncol);
+    const int i = a.i0 + (int)(blockIdx.x / a.ncol);
+    const u32 N = (u32)a.N, N2 = 2 * (u32)a.N;
+    const u32 e = (u32)(((u64)i * a.rho) % N2);
+    if (t < 2) SL[t] = (u32)((long)(a.off + i + (t ? a.h : 0)) * a.NC + col);
+    __syncthreads();
+    Coef st;
+    st.dig = a.dig;
+    st.cb = a.cb;
+    st.top = a.top;
+    unsigned short *CODE = (unsigned short *)smem;
+    Pr x[2][PP];
+    rp_stage_codes<LOADB ? 2 : 1, PP>(CODE, st, SL, t);
+    rp_load_limbs<LOADB ? 2 : 1, 2, PP>(x, st, SL, t);
+    __syncthreads();
+    rp_decode<LOADB ? 2 : 1, 2, PP>(x, CODE, t);
+    // y <- 2^E y through exchange slot 0 (E workgroup-uniform); barriers on both sides
+    auto rot = [&](Pr(&y)[PP], u32 E) {
+        if (E == 0) return;
+        rp_pub<PP>(X, 0, y, t);
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < PP; ++r) {
+            RP_FENCE();
+            if (E % 128 == 0) {
+                bool ng;
+                const Pr v = rp_get_al<PP>(X, 0, t + RP_NT * r, E, N, ng);
+                y[r] = pr_cneg(v, ng);
+            } else {
+                y[r] = rp_get_gen<PP>(X, 0, t + RP_NT * r, E, N);
+            }
+        }
+        __syncthreads();
+    };
+    switch (OP) {
+    case OP_DOUBLE:   // a = 2a
+#pragma unroll
+        for (int r = 0; r < PP; ++r) x[0][r] = pr_add(x[0][r], x[0][r]);
+        break;
+    case OP_HALFADD:  // a = (a + b) / 2
+#pragma unroll
+        for (int r = 0; r < PP; ++r) x[0][r] = pr_add(x[0][r], x[1][r]);
+        rot(x[0], N2 - 1);
+        break;
+    case OP_FILL:     // b = 2^e a
+#pragma unroll
+        for (int r = 0; r < PP; ++r) x[1][r] = x[0][r];
+        rot(x[1], e);
+        break;
+    case OP_FIX:      // d = a - b; a = a + d; b = 2^e d
+#pragma unroll
+        for (int r = 0; r < PP; ++r) {
+            const Pr d = pr_sub(x[0][r], x[1][r]);
+            x[0][r] = pr_add(x[0][r], d);
+            x[1][r] = d;
+        }
+        rot(x[1], e);
+        break;
+    case OP_TWOXMY:   // a = 2a - b
+#pragma unroll
+        for (int r = 0; r < PP; ++r) x[0][r] = pr_sub(pr_add(x[0][r], x[0][r]), x[1][r]);
+        break;
+    default:          // OP_IBFLY: t = 2^-e b; a, b = a + t, a - t
+        rot(x[1], e ? N2 - e : 0);
+#pragma unroll
+        for (int r = 0; r < PP; ++r) pr_bfly(x[0][r], x[1][r], x[0][r], x[1][r], false);
+        break;
+    }
+    __syncthreads();   // HX (rp_store) overlays the exchange slot and the codes
+    rp_store<2, 2, PP>(x, st, SL, [&](int k) -> bool {
+        return k == 0 ? OP != OP_FILL : (OP == OP_FILL || OP == OP_FIX || OP == OP_IBFLY);
+    }, (short *)smem, t);
 }

@@ -31,3 +31,23 @@ rp_fn rp_get(int l, int logg, int dir, int mode)
     }
     return nullptr;
 }
+
+rp_pair_fn rp_pair_get_p1(int op)
+{
+    static const rp_pair_fn tab[6] = {k_rpair<1, OP_DOUBLE>, k_rpair<1, OP_HALFADD>, k_rpair<1, OP_FILL>,
+                                      k_rpair<1, OP_FIX>, k_rpair<1, OP_TWOXMY>, k_rpair<1, OP_IBFLY>};
+    return op >= 0 && op < 6 ? tab[op] : nullptr;
+}
+
+rp_pair_fn rp_pair_get_p2(int op);
+rp_pair_fn rp_pair_get_p4(int op);
+
+rp_pair_fn rp_pair_get(int l, int op)
+{
+    switch (l) {
+    case 1024: return rp_pair_get_p1(op);
+    case 2048: return rp_pair_get_p2(op);
+    case 4096: return rp_pair_get_p4(op);
+    }
+    return nullptr;
+}

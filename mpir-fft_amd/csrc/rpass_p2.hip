@@ -18,3 +18,10 @@ rp_fn rp_get_p2(int logg, int dir, int mode)
     if (logg < 1 || logg > 3 || dir < 0 || dir > 1 || mode < 0 || mode > 2) return nullptr;
     return tab[dir][mode][logg];
 }
+
+rp_pair_fn rp_pair_get_p2(int op)
+{
+    static const rp_pair_fn tab[6] = {k_rpair<2, OP_DOUBLE>, k_rpair<2, OP_HALFADD>, k_rpair<2, OP_FILL>,
+                                      k_rpair<2, OP_FIX>, k_rpair<2, OP_TWOXMY>, k_rpair<2, OP_IBFLY>};
+    return op >= 0 && op < 6 ? tab[op] : nullptr;
+}
