@@ -117,8 +117,12 @@ def pmc_traffic(cfg, kernel):
         return None, None
     with open(p) as f:
         d = json.load(f)
+    want = kernel.split(" ")[0]                    # e.g. "k_pwss<20>" -> matches "void k_pwss<20, 8>(...)"
+    stem, tmpl = want.split("<")[0], want[len(want.split("<")[0]):].strip("<>")
     for name, rec in d.get("kernels", {}).items():
-        if name.startswith(kernel.split(" ")[0].split("<")[0]) and "hbm_bytes_per_launch" in rec:
+        base = name.replace("void ", "").split("(")[0]
+        if base.split("<")[0] == stem and (not tmpl or base.split("<", 1)[-1].startswith(tmpl)) \
+                and "hbm_bytes_per_launch" in rec:
             return rec["hbm_bytes_per_launch"], os.path.relpath(p, ROOT)
     return None, None
 

@@ -53,6 +53,15 @@ void new_mpn_mul(mp_limb_t *r1, mp_limb_t *i1, mp_size_t n1, mp_limb_t *i2, mp_s
 int mpfft_mul_ex(uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i2, long n2,
                  unsigned long depth, unsigned long w);
 
+/* (depth, w) chooser: the reference leaves them to its caller (mul_fft.c:3190-3191).
+ * Picks the valid pair (power-of-two w, coefficients of <= 4096 limbs) with the least
+ * predicted MI355X time (measured table, profiles/r02/chooser_sweep.json).
+ * Returns MPFFT_OK, or MPFFT_ETOOBIG when no supported pair holds the product. */
+int mpfft_choose(long n1, long n2, unsigned long *depth, unsigned long *w);
+
+/* mpn_mul-style entry: r1 = i1 * i2 with (depth, w) from mpfft_choose (host pointers). */
+int mpfft_mul_auto(uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i2, long n2);
+
 /* Free the calling thread's device context buffers (re-allocated by the next call). */
 int mpfft_release(void);
 
@@ -102,6 +111,9 @@ typedef struct mpfft_shard {
     int *col_top[2];
     uint64_t *row_dig[2], *row_cb[2];
     int *row_top[2];
+    long src_chunk;           /* 0: d_i1/d_i2 are the whole operands; else this rank's column
+                                 slices: for each position p < T/NC, `src_chunk` limbs from
+                                 limb floor((p NC + c0) bits1 / 64) on (sharded.py) */
 } mpfft_shard;
 
 #define MPFFT_SHARD_FWD_COLUMNS 0   /* split + column DIF of both operands (column layout) */

@@ -36,7 +36,8 @@ class _Shard(ctypes.Structure):
                 ("c0", ctypes.c_int), ("ccount", ctypes.c_int), ("r0", ctypes.c_int), ("rcount", ctypes.c_int),
                 ("ccb", ctypes.c_int),
                 ("col_dig", ctypes.c_void_p * 2), ("col_cb", ctypes.c_void_p * 2), ("col_top", ctypes.c_void_p * 2),
-                ("row_dig", ctypes.c_void_p * 2), ("row_cb", ctypes.c_void_p * 2), ("row_top", ctypes.c_void_p * 2)]
+                ("row_dig", ctypes.c_void_p * 2), ("row_cb", ctypes.c_void_p * 2), ("row_top", ctypes.c_void_p * 2),
+                ("src_chunk", ctypes.c_long)]
 
 
 class MpfftError(RuntimeError):
@@ -98,6 +99,10 @@ def lib():
         h.mpfft_shard_combine.argtypes = [ctypes.POINTER(_Shard), ctypes.c_int, _vp, _L, _L, _L, _vp, ctypes.c_int,
                                           _vp, ctypes.c_size_t, ctypes.c_int, _vp, _vp]
         h.mpfft_shard_combine.restype = ctypes.c_int
+        h.mpfft_choose.argtypes = [_L, _L, ctypes.POINTER(ctypes.c_ulong), ctypes.POINTER(ctypes.c_ulong)]
+        h.mpfft_choose.restype = ctypes.c_int
+        h.mpfft_mul_auto.argtypes = [_u64p, _u64p, _L, _u64p, _L]
+        h.mpfft_mul_auto.restype = ctypes.c_int
         _lib = h
     return _lib
 
@@ -145,6 +150,27 @@ def mul(i1, i2, depth, w):
     i2 = np.ascontiguousarray(i2, dtype=np.uint64)
     r = np.zeros(len(i1) + len(i2), dtype=np.uint64)
     new_mpn_mul(r, i1, len(i1), i2, len(i2), depth, w)
+    return r
+
+
+def choose(n1, n2):
+    """(depth, w) the library would use for an n1 x n2-limb product (mpfft_choose: the
+    reference leaves them to the caller, mul_fft.c:3190-3191)."""
+    d, w = ctypes.c_ulong(), ctypes.c_ulong()
+    rc = lib().mpfft_choose(n1, n2, ctypes.byref(d), ctypes.byref(w))
+    if rc:
+        raise MpfftError(rc, f"choose(n1={n1}, n2={n2})")
+    return int(d.value), int(w.value)
+
+
+def mul_auto(i1, i2):
+    """mpn_mul-style product with (depth, w) from choose(): a new uint64 array of n1+n2 limbs."""
+    i1 = np.ascontiguousarray(i1, dtype=np.uint64)
+    i2 = np.ascontiguousarray(i2, dtype=np.uint64)
+    r = np.zeros(len(i1) + len(i2), dtype=np.uint64)
+    rc = lib().mpfft_mul_auto(_p(r), _p(i1), len(i1), _p(i2), len(i2))
+    if rc:
+        raise MpfftError(rc, f"mul_auto(n1={len(i1)}, n2={len(i2)})")
     return r
 
 
@@ -258,6 +284,7 @@ def shard_desc(sh):
         d.row_dig[k] = sh["row"][k]["dig"].data_ptr()
         d.row_cb[k] = sh["row"][k]["cb"].data_ptr()
         d.row_top[k] = sh["row"][k]["top"].data_ptr()
+    d.src_chunk = int(sh.get("src_chunk", 0))
     return d
 
 

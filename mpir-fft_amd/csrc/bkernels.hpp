@@ -463,9 +463,10 @@ __global__ __launch_bounds__(64 * BP_WAVES) void k_bpass(PassArgs a)
                     const long ns = a.nsrc[op];
                     const u64 *sp = a.src[op];
                     if ((u64)pp * 128 < a.bits1) {
-                        v[kk].x = q < ns ? sp[q] : 0;
-                        v[kk].y = q + 1 < ns ? sp[q + 1] : 0;
-                        x2[kk] = q + 2 < ns ? sp[q + 2] : 0;
+                        const SrcSlice sv{a.src_chunk, a.jNC, a.sub_off};
+                        v[kk].x = src_limb(sp, ns, sv, j, a.bits1, q);
+                        v[kk].y = src_limb(sp, ns, sv, j, a.bits1, q + 1);
+                        x2[kk] = src_limb(sp, ns, sv, j, a.bits1, q + 2);
                     }
                 } else {
                     const long sl = slot_of(i);

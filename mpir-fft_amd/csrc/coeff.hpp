@@ -571,11 +571,30 @@ __device__ __forceinline__ void zero_coeff(i64 (&d)[2 * U])
     for (int k = 0; k < 2 * U; ++k) d[k] = 0;
 }
 
+// Where the fused split reads the operand: the whole operand (chunk == 0), or one rank's
+// column slice of it (multi-GPU, sharded.py): for every MFA position p the limbs from
+// floor((p NC + c0) bits1 / 64) on, `chunk` of them per position, back to back.
+struct SrcSlice {
+    long chunk;   // limbs per position, 0 = whole operand
+    long NC;      // columns (a power of two)
+    long c0;      // first column of the slice
+};
+
+// limb q of the operand as seen by coefficient j = p NC + c (bits past its end read as 0)
+__device__ __forceinline__ u64 src_limb(const u64 *src, long nsrc, const SrcSlice &v, long j, u64 bits1, long q)
+{
+    if (q >= nsrc) return 0;
+    if (!v.chunk) return src[q];
+    const long p = j >> __builtin_ctzl((unsigned long)v.NC);
+    const long r = q - (long)(((u64)(p * v.NC + v.c0) * bits1) >> 6);   // >= 0 for the slice's coefficients
+    return r < v.chunk ? src[p * v.chunk + r] : 0;
+}
+
 // Fused split (FFT_split_bits, mul_fft.c:115-170): coefficient j is the bits1-bit
 // chunk at bit offset j*bits1 of the operand (bits past its end read as 0).
 template <int U>
 __device__ __forceinline__ void load_split(const WG &c, i64 (&d)[2 * U], const u64 *src, long nsrc,
-                                           long j, u64 bits1, int l)
+                                           const SrcSlice &sv, long j, u64 bits1, int l)
 {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -585,8 +604,8 @@ __device__ __forceinline__ void load_split(const WG &c, i64 (&d)[2 * U], const u
             u64 off = (u64)j * bits1 + (u64)m * 64;
             long q = (long)(off >> 6);
             int s = (int)(off & 63);
-            u64 w0 = (q < nsrc) ? src[q] : 0;
-            u64 w1 = (s && q + 1 < nsrc) ? src[q + 1] : 0;
+            u64 w0 = src_limb(src, nsrc, sv, j, bits1, q);
+            u64 w1 = s ? src_limb(src, nsrc, sv, j, bits1, q + 1) : 0;
             v = s ? (w0 >> s) | (w1 << (64 - s)) : w0;
             u64 left = bits1 - (u64)m * 64;
             if (left < 64) v &= (((u64)1) << left) - 1;

@@ -28,6 +28,7 @@ struct PassArgs {
     int *top[2];
     const u64 *src[2];   // non-null: load coefficients straight from the operand (fused split)
     long nsrc[2];
+    long src_chunk;      // 0: src is the whole operand; else the rank's column slice (src_limb, sharded.py)
     u64 bits1;
     u64 N;               // bits
     int l;               // limbs
@@ -192,7 +193,7 @@ __global__ __launch_bounds__(MPF_LB(U)) void k_pass(PassArgs a)
     for (int i = 0; i < G; ++i) {
         if (DIR == 0 && pos0 + i * pstep >= a.zero_from) zero_coeff<U>(x[i]);
         else if (a.src[op])
-            load_split<U>(c, x[i], a.src[op], a.nsrc[op],
+            load_split<U>(c, x[i], a.src[op], a.nsrc[op], SrcSlice{a.src_chunk, a.jNC, a.sub_off},
                           (long)(a.pos_off + pos0 + i * pstep) * a.jNC + a.sub_off + sub, a.bits1, l);
         else load_coeff<U>(c, x[i], st, slot_of(i), l);
     }

@@ -139,7 +139,7 @@ __global__ __launch_bounds__(32 << LOGG) void k_lpass(PassArgs a)
             for (int c = 0; c < 2; ++c) {
                 const int i = 2 * q + c;
                 if (DIR == 0 && pos0 + i * pstep >= a.zero_from) zero_coeff<U>(x[c]);
-                else wv_load_split<U, F>(x[c], a.src[op], a.nsrc[op],
+                else wv_load_split<U, F>(x[c], a.src[op], a.nsrc[op], SrcSlice{a.src_chunk, a.jNC, a.sub_off},
                                          (long)(a.pos_off + pos0 + i * pstep) * a.jNC + a.sub_off + sub, a.bits1, l,
                                          lane);
             }

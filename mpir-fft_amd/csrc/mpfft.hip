@@ -245,6 +245,7 @@ struct Exec {
     View col, row;
     int c0, ccount, r0, rcount, ccb, cbb;
     long cbs;
+    long src_chunk = 0;      // operands are column slices (mpfft_shard.src_chunk), 0 = whole operands
     u32 *zflags = nullptr;   // non-null: the first forward column pass clears the combine's look-back flags
     long zflags_n = 0;       // (u32 words), so combine_single needs no separate fill launch
 
@@ -475,6 +476,7 @@ struct Exec {
             if (lvl == 0) {
                 a.src[0] = srcA; a.nsrc[0] = nA;
                 a.src[1] = srcB; a.nsrc[1] = nB;
+                a.src_chunk = src_chunk;
                 a.zero_from = (int)P.Tr;
                 a.zp = zflags;
                 a.zn = zflags_n;
@@ -1083,6 +1085,7 @@ static int shard_exec(Exec &X, const mpfft_shard *sh)
     X.ccb = sh->ccb;
     X.cbb = ilog2(sh->ccb);
     X.cbs = (long)sh->rcount * sh->ccb;
+    X.src_chunk = sh->src_chunk;
     return MPFFT_OK;
 }
 
@@ -1199,6 +1202,53 @@ int mpfft_release(void)
     C.io = nullptr;
     C.ws_bytes = C.io_bytes = 0;
     return MPFFT_OK;
+}
+
+// ---- (depth, w) chooser -------------------------------------------
+// The reference leaves (depth, w) to its caller (mul_fft.c:3190-3191); an MPIR-style
+// mpn_mul drop-in needs them picked from the operand sizes.  Candidates: every depth in
+// [2, 24] and power-of-two w with a whole number of limbs per coefficient, l <= 4096, and
+// room for the product (make_plan).  Predicted device time = launches x a launch cost +
+// live slots (T) x the measured per-slot cost of a multiply at that coefficient size
+// (CHOOSE_SLOT_NS[log2 l], from scripts/chooser_sweep.py on MI355X:
+// profiles/r02/chooser_sweep.json); the cheapest candidate wins.  Model: a fixed cost
+// (launches: ~0.045 ms for the small configurations of the sweep) + T x the marginal
+// per-slot cost at that coefficient size, (ms - 0.045) / T of the sweep.
+static const double CHOOSE_SLOT_NS[13] = {69.7, 26.6, 12.3, 10.4, 7.3, 6.6, 11.0, 13.2, 28.4, 98.2, 167.9, 270.0, 810.7};
+static const double CHOOSE_FIXED_MS = 0.045;
+
+static double choose_cost(const Plan &P)
+{
+    const int k = ilog2(P.l);
+    return CHOOSE_FIXED_MS + (double)P.trunc * CHOOSE_SLOT_NS[k < 12 ? k : 12] * 1e-6;
+}
+
+int mpfft_choose(long n1, long n2, unsigned long *depth, unsigned long *w)
+{
+    double best = -1.0;
+    for (unsigned long d = 2; d <= 24; ++d)
+        for (unsigned long wv = 1; wv <= 4096; wv *= 2) {
+            const unsigned long long N = (1ull << d) * wv;
+            if (N % 64) continue;
+            if (N / 64 > 4096) break;
+            Plan P;
+            if (make_plan(&P, n1, n2, d, wv)) continue;
+            const double c = choose_cost(P);
+            if (best < 0 || c < best) {
+                best = c;
+                *depth = d;
+                *w = wv;
+            }
+        }
+    return best < 0 ? MPFFT_ETOOBIG : MPFFT_OK;
+}
+
+int mpfft_mul_auto(uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i2, long n2)
+{
+    unsigned long d = 0, wv = 0;
+    const int rc = mpfft_choose(n1, n2, &d, &wv);
+    if (rc) return rc;
+    return mpfft_mul_ex(r1, i1, n1, i2, n2, d, wv);
 }
 
 // mul_fft.c:3190 -- same signature and meaning; fails loudly instead of segfaulting

@@ -503,7 +503,9 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
                 const long q = (long)(off >> 6);
                 const int sh = (int)(off & 63);
                 const long ns = left ? a.nsrc[op] : 0;
-                const u64 x0 = q < ns ? src[q] : 0, x1 = q + 1 < ns ? src[q + 1] : 0, x2 = q + 2 < ns ? src[q + 2] : 0;
+                const SrcSlice sv{a.src_chunk, a.jNC, a.sub_off};
+                const u64 x0 = src_limb(src, ns, sv, j, a.bits1, q), x1 = src_limb(src, ns, sv, j, a.bits1, q + 1),
+                          x2 = src_limb(src, ns, sv, j, a.bits1, q + 2);
                 u64 f0 = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
                 u64 f1 = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
                 f0 = left < 64 ? f0 & ((((u64)1) << left) - 1) : f0;

@@ -117,8 +117,8 @@ __device__ __forceinline__ void wv_load(i64 (&d)[2 * U], const Coef &s, long slo
 
 // fused split (FFT_split_bits, mul_fft.c:115-170)
 template <int U, bool F>
-__device__ __forceinline__ void wv_load_split(i64 (&d)[2 * U], const u64 *src, long nsrc, long j, u64 bits1, int l,
-                                              int lane)
+__device__ __forceinline__ void wv_load_split(i64 (&d)[2 * U], const u64 *src, long nsrc, const SrcSlice &sv, long j,
+                                              u64 bits1, int l, int lane)
 {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -128,8 +128,8 @@ __device__ __forceinline__ void wv_load_split(i64 (&d)[2 * U], const u64 *src, l
             const u64 off = (u64)j * bits1 + (u64)m * 64;
             const long q = (long)(off >> 6);
             const int s = (int)(off & 63);
-            const u64 w0 = (q < nsrc) ? src[q] : 0;
-            const u64 w1 = (s && q + 1 < nsrc) ? src[q + 1] : 0;
+            const u64 w0 = src_limb(src, nsrc, sv, j, bits1, q);
+            const u64 w1 = s ? src_limb(src, nsrc, sv, j, bits1, q + 1) : 0;
             v = s ? (w0 >> s) | (w1 << (64 - s)) : w0;
             const u64 left = bits1 - (u64)m * 64;
             if (left < 64) v &= (((u64)1) << left) - 1;

@@ -133,7 +133,7 @@ __global__ __launch_bounds__(64 * WPB) void k_wpass(PassArgs a)
 #pragma unroll
         for (int i = 0; i < G; ++i) {
             if (DIR == 0 && pos0 + i * pstep >= a.zero_from) zero_coeff<U>(x[i]);
-            else wv_load_split<U, F>(x[i], a.src[op], a.nsrc[op],
+            else wv_load_split<U, F>(x[i], a.src[op], a.nsrc[op], SrcSlice{a.src_chunk, a.jNC, a.sub_off},
                                      (long)(a.pos_off + pos0 + i * pstep) * a.jNC + a.sub_off + sub, a.bits1, l, lane);
         }
     } else {

@@ -60,6 +60,24 @@ class ShardPlan:
             if self.rows[d + 1] - self.rows[d] < 1:
                 raise ValueError("a rank owns no rows")
 
+        # operand column slices (fused split reads them through SrcSlice, coeff.hpp): for
+        # each live position p < Tr, limbs from floor((p NC + c0) bits1 / 64) on
+        self.chunk = (self.C * self.bits1 + 63) // 64 + 2
+
+    def slice_start(self, p, d):
+        return ((p * self.NC + d * self.C) * self.bits1) // 64
+
+    def slice_operand(self, a, d):
+        """rank d's column slice of operand a (uint64 limbs): Tr chunks of `chunk` limbs."""
+        out = np.zeros(self.Tr * self.chunk, dtype=np.uint64)
+        for p in range(self.Tr):
+            s0 = self.slice_start(p, d)
+            if s0 >= len(a):
+                break
+            seg = a[s0: s0 + self.chunk]
+            out[p * self.chunk: p * self.chunk + len(seg)] = seg
+        return out
+
     def rcount(self, d):
         return self.rows[d + 1] - self.rows[d]
 
@@ -74,8 +92,9 @@ class ShardedMul:
     """One rank's part.  `backend` runs the stages on this rank's buffers,
     `comm` moves them (both duck-typed; see GpuBackend / TorchComm)."""
 
-    def __init__(self, plan, rank, backend, comm):
+    def __init__(self, plan, rank, backend, comm, sliced=True):
         self.p, self.rank, self.be, self.comm = plan, rank, backend, comm
+        self.sliced = sliced          # run() gets this rank's operand slices (ShardPlan.slice_operand)
         p = plan
         self.col = [backend.alloc_coeffs(p.col_slots()) for _ in range(2)]
         self.row = [backend.alloc_coeffs(p.row_slots(rank)) for _ in range(2)]
@@ -83,40 +102,48 @@ class ShardedMul:
     def shard_desc(self):
         p, d = self.p, self.rank
         return dict(n1=p.n1, n2=p.n2, depth=p.depth, w=p.w, c0=d * p.C, ccount=p.C,
-                    r0=p.rows[d], rcount=p.rcount(d), ccb=p.C, col=self.col, row=self.row)
+                    r0=p.rows[d], rcount=p.rcount(d), ccb=p.C, col=self.col, row=self.row,
+                    src_chunk=p.chunk if self.sliced else 0)
 
-    # all-to-all #1 / #3: column layout rows [r_d, r_{d+1}) -> rank d's row layout block
-    def _col_to_row(self, k, fields):
-        p = self.p
-        ins = [p.rcount(d) * p.C for d in range(p.world)]            # slots sent to each rank
-        outs = [p.rcount(self.rank) * p.C] * p.world                  # slots received from each rank
-        n_in = sum(ins)
-        for f in fields:
-            self.comm.all_to_all(self.row[k][f], self.col[k][f][: n_in * self.be.width(f, p)],
-                                 [s * self.be.width(f, p) for s in outs], [s * self.be.width(f, p) for s in ins])
+    # all-to-all #1 / #3: column layout rows [r_d, r_{d+1}) -> rank d's row layout block;
+    # every field (and operand) of one exchange goes in one batch of point-to-point ops
+    def _col_to_row(self, ks, fields):
+        p, me = self.p, self.rank
+        plan = []
+        for k in ks:
+            for f in fields:
+                wd = self.be.width(f, p)
+                send = [self.col[k][f][p.rows[d] * p.C * wd: p.rows[d + 1] * p.C * wd] for d in range(p.world)]
+                blk = p.rcount(me) * p.C * wd
+                recv = [self.row[k][f][s * blk: (s + 1) * blk] for s in range(p.world)]
+                plan.append((send, recv))
+        self.comm.exchange(plan)
 
     # all-to-all #2: row layout block s -> rank s's column layout rows [r_d, r_{d+1})
-    def _row_to_col(self, k, fields):
-        p = self.p
-        ins = [p.rcount(self.rank) * p.C] * p.world
-        outs = [p.rcount(d) * p.C for d in range(p.world)]
-        n_out = sum(outs)
-        for f in fields:
-            self.comm.all_to_all(self.col[k][f][: n_out * self.be.width(f, p)], self.row[k][f],
-                                 [s * self.be.width(f, p) for s in outs], [s * self.be.width(f, p) for s in ins])
+    def _row_to_col(self, ks, fields):
+        p, me = self.p, self.rank
+        plan = []
+        for k in ks:
+            for f in fields:
+                wd = self.be.width(f, p)
+                blk = p.rcount(me) * p.C * wd
+                send = [self.row[k][f][s * blk: (s + 1) * blk] for s in range(p.world)]
+                recv = [self.col[k][f][p.rows[d] * p.C * wd: p.rows[d + 1] * p.C * wd] for d in range(p.world)]
+                plan.append((send, recv))
+        self.comm.exchange(plan)
 
     def run(self, i1, i2):
-        """i1, i2: full operands on this rank (backend arrays).  Returns (m0, limbs)."""
+        """i1, i2: this rank's operand column slices (ShardPlan.slice_operand; the full
+        operands when sliced=False), backend arrays.  Returns (m0, limbs)."""
         p, be, sh = self.p, self.be, self.shard_desc()
         be.stage("fwd_columns", sh, i1, i2)
-        for k in (0, 1):
-            self._col_to_row(k, ("dig", "cb", "top"))
+        self._col_to_row((0, 1), ("dig", "cb", "top"))
         be.stage("fwd_rows", sh, i1, i2)
         be.stage("pointwise", sh, i1, i2)
         be.stage("inv_rows", sh, i1, i2)
-        self._row_to_col(0, ("dig", "cb", "top"))
+        self._row_to_col((0,), ("dig", "cb", "top"))
         be.stage("inv_columns", sh, i1, i2)
-        self._col_to_row(0, ("dig",))                      # canonical coefficients: limbs only
+        self._col_to_row((0,), ("dig",))                   # canonical coefficients: limbs only
         # halo: the last H coefficients of every rank's range, all-gathered
         halo_all = self.comm.all_gather(be.tail_coeffs(sh, p.H))
         d = self.rank
@@ -131,6 +158,11 @@ class ShardedMul:
             cin = 1 if (g or (pr and cin)) else 0
         limbs = be.combine(sh, 1, m0, mcount, kbase, halo, p.H if d else 0, cin=cin)
         return m0, limbs
+
+
+def torch_empty_like_cpu(t):
+    import torch
+    return torch.empty(t.shape, dtype=t.dtype)
 
 
 class TorchComm:
@@ -149,6 +181,32 @@ class TorchComm:
             out.copy_(o)
         else:
             self.dist.all_to_all_single(out, inp, out_splits, in_splits)
+
+    def exchange(self, plan):
+        """plan: [(send views by peer, recv views by peer)]; one batch of isend/irecv for
+        all of them (one RCCL group on GPUs), the rank's own views copied locally."""
+        me = self.dist.get_rank()
+        ops, back = [], []
+        for send, recv in plan:
+            recv[me].copy_(send[me])
+            for d in range(len(send)):
+                if d == me:
+                    continue
+                sv, rv = send[d], recv[d]
+                if self.host and sv.is_cuda:
+                    sv = sv.cpu()
+                    rh = torch_empty_like_cpu(rv)
+                    back.append((rv, rh))
+                    rv = rh
+                if sv.numel():
+                    ops.append(self.dist.P2POp(self.dist.isend, sv.contiguous(), d))
+                if rv.numel():
+                    ops.append(self.dist.P2POp(self.dist.irecv, rv, d))
+        if ops:
+            for r in self.dist.batch_isend_irecv(ops):
+                r.wait()
+        for dst, h in back:
+            dst.copy_(h)
 
     def all_gather(self, t):
         import torch
@@ -229,8 +287,10 @@ def bench(args, cfg_name, cfg, rank, world, dev):
     plan = ShardPlan(mp, nl, nl, depth, w, world)
     a = mp.fill_random(nl, 0x1001)
     b = mp.fill_random(nl, 0x2002)
-    da = torch.from_numpy(a.view(np.int64)).to(dev)
-    db = torch.from_numpy(b.view(np.int64)).to(dev)
+    # only this rank's column slices of the operands travel to its GPU (1/world of each)
+    da = torch.from_numpy(plan.slice_operand(a, rank).view(np.int64)).to(dev)
+    db = torch.from_numpy(plan.slice_operand(b, rank).view(np.int64)).to(dev)
+    del a, b
     be = GpuBackend(mp, plan, dev)
     comm = TorchComm(host_staging=(world > 1 and dist.get_backend() != "nccl")) if world > 1 else _SoloComm()
     job = ShardedMul(plan, rank, be, comm)
@@ -282,7 +342,7 @@ def bench(args, cfg_name, cfg, rank, world, dev):
             "data": "synthetic (xoshiro256** limbs, seeds 0x1001/0x2002)",
             "config": {"workload": f"{cfg_name}: sharded new_mpn_mul depth={depth} w={w} n1=n2={nl} limbs "
                                    f"(l={P['l']}, NC x NR = {P['NC']} x {P['NR']}, trunc={P['trunc']})",
-                       "parallelism": f"MFA columns x{world}, 3 all-to-all + halo all-gather "
+                       "parallelism": f"MFA columns x{world}, operand column slices, 3 batched point-to-point exchanges + halo all-gather "
                                       f"({'RCCL' if world > 1 and dist.get_backend() == 'nccl' else 'local'})"},
             "pipeline": {"b_alg_bytes": balg,
                          "hbm_frac_b_alg": balg / (el / args.steps) / (world * 8.0e12),
@@ -292,6 +352,10 @@ def bench(args, cfg_name, cfg, rank, world, dev):
 
 class _SoloComm:
     """world == 1: exchanges are local copies."""
+
+    def exchange(self, plan):
+        for send, recv in plan:
+            recv[0].copy_(send[0])
 
     def all_to_all(self, out, inp, out_splits, in_splits):
         out[: inp.numel()].copy_(inp)

@@ -68,11 +68,16 @@ class MockBackend:
     def _fwd_columns(self, sh, i1, i2):
         p = self.p
         mask = (1 << p.bits1) - 1
+        ch = sh.get("src_chunk", 0)
         for k, op in ((0, i1), (1, i2)):
             X = int.from_bytes(op.numpy().view(np.uint64).tobytes(), "little")
             for cl in range(sh["ccount"]):
                 c = sh["c0"] + cl
-                xs = [(X >> ((jr * p.NC + c) * p.bits1)) & mask for jr in range(p.Tr)]
+                if ch:   # column slice: position jr's chunk starts at limb floor((jr NC + c0) bits1 / 64)
+                    xs = [(X >> (64 * jr * ch + (jr * p.NC + c) * p.bits1 - 64 * p.slice_start(jr, sh["c0"] // p.C)))
+                          & mask for jr in range(p.Tr)]
+                else:
+                    xs = [(X >> ((jr * p.NC + c) * p.bits1)) & mask for jr in range(p.Tr)]
                 for pos in range(p.NR):
                     kr = revbin(pos, self.lbR)
                     v = sum(x * self.pw(p.w * p.NC * jr * kr) for jr, x in enumerate(xs) if x)

@@ -239,3 +239,15 @@ def test_c2_c3_exact_vs_gmp(mp, oracle):
         b = mp.fill_random(nl, 0x2002)
         got = mp.mul(a, b, depth, w)
         assert (got == oracle.gmp_mul(a, b)).all()
+
+
+def test_mul_auto_exact_across_sizes(mp, oracle):
+    """mpn_mul-style entry with the chooser's (depth, w): exact products from 1e3- to
+    1e9-bit operands (balanced and unbalanced) against GMP mpn_mul."""
+    rng = random.Random(91)
+    for n in (16, 157, 1000, 4096, 31250, 10**5, 10**6, 15625000):
+        for n2 in (n, max(1, n // 5)):
+            a = mp.fill_random(n, rng.getrandbits(64))
+            b = mp.fill_random(n2, rng.getrandbits(64))
+            got = mp.mul_auto(a, b)
+            assert (got == oracle.gmp_mul(a, b)).all(), (n, n2, mp.choose(n, n2))

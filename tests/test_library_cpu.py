@@ -75,3 +75,17 @@ def test_compute_fails_loudly_without_gpu(mp):
 def test_prng_matches_oracle(mp, oracle):
     for seed in (0x1001, 0x2002, 7):
         assert (mp.fill_random(1000, seed) == oracle.fill_random(1000, seed)).all()
+
+
+def test_chooser_picks_valid_parameters(mp):
+    """mpfft_choose (the reference leaves (depth, w) to the caller,
+    mul_fft.c:3190-3191): every pick is a valid, supported plan that holds the product,
+    across 1e3- to 1e10-bit operands, balanced and unbalanced."""
+    sizes = [1, 2, 16, 100, 1000, 16384, 10**5, 261952, 10**6, 15625000, 20312500, 156250000]
+    for n1 in sizes:
+        for n2 in (n1, max(1, n1 // 7), 3):
+            d, w = mp.choose(n1, n2)
+            assert w & (w - 1) == 0 and ((1 << d) * w) % 64 == 0
+            assert mp.check_params(n1, n2, d, w) == 0, (n1, n2, d, w)
+    with pytest.raises(mp.MpfftError):
+        mp.choose(10**12, 10**12)                       # beyond 4096-limb coefficients at depth 24

@@ -42,7 +42,8 @@ def _worker(rank, world, port, depth, w, n1, n2, seed, q):
         a = mp.fill_random(n1, rng.getrandbits(64))
         b = mp.fill_random(n2, rng.getrandbits(64))
         job = ShardedMul(plan, rank, MockBackend(plan), TorchComm())
-        m0, limbs = job.run(torch.from_numpy(a.view(np.int64)), torch.from_numpy(b.view(np.int64)))
+        sa, sb = plan.slice_operand(a, rank), plan.slice_operand(b, rank)   # this rank's column slices
+        m0, limbs = job.run(torch.from_numpy(sa.view(np.int64)), torch.from_numpy(sb.view(np.int64)))
         # gather the distributed product on every rank
         sizes = [plan.M[d + 1] - plan.M[d] for d in range(world)]
         pad = torch.zeros(max(sizes), dtype=torch.int64)

@@ -30,7 +30,8 @@ def test_sharded_world1(mp, depth, w, n1, n2):
     a = mp.fill_random(n1, 5 + depth)
     b = mp.fill_random(n2, 6 + w)
     job = ShardedMul(plan, 0, GpuBackend(mp, plan, dev), _SoloComm())
-    m0, limbs = job.run(torch.from_numpy(a.view(np.int64)).to(dev), torch.from_numpy(b.view(np.int64)).to(dev))
+    sa, sb = plan.slice_operand(a, 0), plan.slice_operand(b, 0)
+    m0, limbs = job.run(torch.from_numpy(sa.view(np.int64)).to(dev), torch.from_numpy(sb.view(np.int64)).to(dev))
     torch.cuda.synchronize()
     assert m0 == 0 and _exact(a, b, limbs.cpu().numpy())
 
@@ -61,7 +62,8 @@ def _worker(rank, world, port, depth, w, n1, n2, q):
         a = mp.fill_random(n1, 0x1001)
         b = mp.fill_random(n2, 0x2002)
         job = ShardedMul(plan, rank, GpuBackend(mp, plan, dev), TorchComm(host_staging=True))
-        m0, limbs = job.run(torch.from_numpy(a.view(np.int64)).to(dev), torch.from_numpy(b.view(np.int64)).to(dev))
+        sa, sb = plan.slice_operand(a, rank), plan.slice_operand(b, rank)   # this rank's column slices
+        m0, limbs = job.run(torch.from_numpy(sa.view(np.int64)).to(dev), torch.from_numpy(sb.view(np.int64)).to(dev))
         limbs = limbs.cpu()
         sizes = [plan.M[d + 1] - plan.M[d] for d in range(world)]
         pad = torch.zeros(max(sizes), dtype=torch.int64)
