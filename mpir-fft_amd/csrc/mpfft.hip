@@ -755,6 +755,14 @@ struct Exec {
     {
         const long cnt = (long)P.Tr * ccount;
         if (P.fuse_scale) return MPFFT_OK;   // done by the last inverse column pass
+        if (P.rpass) {   // register-resident scale + canonicalisation (rkernels.hpp)
+            rp_scale_fn f = rp_scale_get((int)P.l);
+            if (!f) return MPFFT_EUNSUPPORTED;
+            hipLaunchKernelGGL(f, dim3((unsigned)cnt), dim3(RP_NT), rp_scale_lds((int)P.l), s, col.dig[0], col.cb[0],
+                               col.top[0], (unsigned)P.N, (unsigned)(2 * P.N - (u64)(P.depth + 1)));
+            HIPCHK(hipGetLastError());
+            return MPFFT_OK;
+        }
         if (P.wave) {
             wv_scale_fn f = wv_fns(P.wU, P.wfull).scale;
             const size_t lds = (size_t)WPB * 16 * P.l;
@@ -934,7 +942,7 @@ int mpfft_stage_kernels(long n1, long n2, unsigned long depth, unsigned long w, 
     else
         snprintf(pw, sizeof pw, "k_pointwise (VALU)");
     const char *pair = P.rpass ? "k_rpair" : P.wave ? "k_wpair" : "k_pairop";
-    const char *scale = P.fuse_scale ? "(fused into the last inverse column pass)" : P.wave ? "k_wscale" : "k_scale";
+    const char *scale = P.fuse_scale ? "(fused into the last inverse column pass)" : P.rpass ? "k_rscale" : P.wave ? "k_wscale" : "k_scale";
     static const bool multi = [] { const char *e = getenv("MPFFT_COMBINE"); return e && !strcmp(e, "multi"); }();
     snprintf(buf, len, "%s;%s;%s;%s;%s + %s;%s;%s", pass, rows, pw, pass, pass, pair, scale,
              multi ? "k_comb_sum + k_carry_*" : "k_combine1");

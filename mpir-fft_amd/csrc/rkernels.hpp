@@ -39,6 +39,17 @@ typedef unsigned long long rp_v2u __attribute__((ext_vector_type(2)));
 // VGPRs or a 64-bit carry mask in SGPRs; the coefficients already take 80 of the 128 VGPRs)
 #define RP_FENCE() do { asm volatile("" ::: "memory"); __builtin_amdgcn_sched_barrier(0); } while (0)
 
+__device__ __forceinline__ u32 rp_uniform(u32 v) { return (u32)__builtin_amdgcn_readfirstlane((int)v); }
+
+// an opaque copy of the thread index: addresses derived from it in one phase are not
+// CSE'd with (and kept live from) another phase -- recomputing them is a few VALU ops,
+// keeping them costs the VGPRs the coefficients need
+__device__ __forceinline__ int rp_launder(int t)
+{
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
 typedef unsigned int rp_v4u __attribute__((ext_vector_type(4)));
 
 struct Pr {
@@ -236,6 +247,7 @@ __device__ __forceinline__ u32 rp_pend(const PassArgs &a, const BGeo &g, int don
 template <int G, int PP, int NX, typename EF>
 __device__ __forceinline__ void rp_rot_all(Pr (&x)[G][PP], const RX<PP> &X, EF efn, u32 N, int t)
 {
+    t = rp_launder(t);
 #pragma unroll
     for (int i0 = 0; i0 < G; i0 += NX) {
 #pragma unroll
@@ -283,12 +295,13 @@ __device__ __forceinline__ u32 rp_exp_entry(const PassArgs &a, const BGeo &g, in
     return tw ? N2 - tw : 0;
 }
 
-__device__ __forceinline__ u32 rp_uniform(u32 v) { return (u32)__builtin_amdgcn_readfirstlane((int)v); }
+
 
 // x_i <- 2^E(i) x_i for all G slots, every E a whole number of limb pairs
 template <int G, int PP, int NX, typename EF>
 __device__ __forceinline__ void rp_rot_all_al(Pr (&x)[G][PP], const RX<PP> &X, EF efn, u32 N, int t)
 {
+    t = rp_launder(t);
 #pragma unroll
     for (int i0 = 0; i0 < G; i0 += NX) {
 #pragma unroll
@@ -365,6 +378,7 @@ template <int NS, int NSX, int PP>
 __device__ __forceinline__ void rp_decode(Pr (&x)[NSX][PP], const unsigned short *CODE, int t)
 {
     constexpr int HP = 512 * PP;
+    t = rp_launder(t);
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
 #pragma unroll
@@ -388,6 +402,7 @@ template <int NS, int NSX, int PP, typename KEEP>
 __device__ __forceinline__ void rp_store(Pr (&x)[NSX][PP], const Coef &st, const u32 *SL, KEEP keep, short *HX, int t)
 {
     constexpr int l = 1024 * PP, HP = l / 2, cbw = 2 * l / 64;
+    t = rp_launder(t);
 #pragma unroll
     for (int i = 0; i < NS; ++i)
 #pragma unroll
@@ -472,7 +487,6 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
     if (t < NEXP) EXPT[t] = rp_exp_entry<LOGG, DIR, GX>(a, g, t, N2);
     else if (t < NEXP + G) SLT[t - NEXP] = (u32)slot_lane(t - NEXP);
     __syncthreads();
-    auto slot_of_t = [&](int i) -> long { return (long)rp_uniform(SLT[i]); };
     const u64 *src = SPLIT ? a.src[op] : nullptr;
     // diagnostics (MPFFT_RP_STAMPS): thread 0 stamps the phase boundaries of this workgroup
     unsigned long long *stamp = a.dbg ? a.dbg + 8 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x) : nullptr;
@@ -524,10 +538,11 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
     for (int li = 0; li < LOGG; ++li) {
         const int JB = DIR == 0 ? LOGG - 1 - li : li;
         // partner x_k read rotated by E: (x_i, x_k) <- (x_i + 2^E x_k, x_i - 2^E x_k)
+        const int tl = rp_launder(t);
 #pragma unroll
         for (int pi = 0; pi < G / 2; ++pi) {
             const int i = ((pi >> JB) << (JB + 1)) | (pi & ((1 << JB) - 1));
-            rp_pub<PP>(X, pi, x[i | (1 << JB)], t);
+            rp_pub<PP>(X, pi, x[i | (1 << JB)], tl);
         }
         __syncthreads();
 #pragma unroll
@@ -539,7 +554,7 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
             for (int r = 0; r < PP; ++r) {
                 if (r % 2 == 0) RP_FENCE();   // two partner reads in flight at a time
                 bool ng;
-                const Pr y = rp_get_al<PP>(X, pi, t + RP_NT * r, E, N, ng);
+                const Pr y = rp_get_al<PP>(X, pi, tl + RP_NT * r, E, N, ng);
                 pr_bfly(x[i][r], x[k][r], x[i][r], y, ng);
             }
         }
@@ -654,4 +669,70 @@ __global__ __launch_bounds__(RP_NT) void k_rpair(PairArgs a)
     rp_store<2, 2, PP>(x, st, SL, [&](int k) -> bool {
         return k == 0 ? OP != OP_FILL : (OP == OP_FILL || OP == OP_FIX || OP == OP_IBFLY);
     }, (short *)smem, t);
+}
+
+// ---- scaling by 2^-(depth+1) and canonicalisation (mul_fft.c:3256-3260) ----------------
+// k_rscale<PP>: one coefficient per workgroup (many per CU, so one's load overlaps
+// another's arithmetic): load into the register pair form, multiply by 2^e with one general
+// rotation through LDS, then resolve every carry: the limbs go back to LDS in the k_bpass
+// slot form (limb + carry into it) and one wave sweeps the rows (bp_canon, the ballot
+// carry-lookahead of mpn_normmod_2expp1 :272) while the other waves wait; the canonical
+// residue in [0, 2^N] is stored with zero carry masks and its carry limb.
+template <int PP>
+__global__ __launch_bounds__(RP_NT) void k_rscale(u64 *dig, u64 *cb, int *top, u32 N, u32 e)
+{
+    constexpr int l = 1024 * PP, HP = l / 2, cbw = 2 * l / 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const RX<PP> X{smem};
+    u32 *SL = (u32 *)(smem + RX<PP>::SB);
+    const int t = threadIdx.x;
+    if (t == 0) SL[0] = blockIdx.x;
+    __syncthreads();
+    Coef st;
+    st.dig = dig;
+    st.cb = cb;
+    st.top = top;
+    unsigned short *CODE = (unsigned short *)smem;
+    Pr x[1][PP];
+    rp_stage_codes<1, PP>(CODE, st, SL, t);
+    rp_load_limbs<1, 1, PP>(x, st, SL, t);
+    __syncthreads();
+    rp_decode<1, 1, PP>(x, CODE, t);
+    rp_pub<PP>(X, 0, x[0], t);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < PP; ++r) x[0][r] = rp_get_gen<PP>(X, 0, t + RP_NT * r, e, N);
+    __syncthreads();
+    // k_bpass slot form: f_m, c_m = carry into limb m (the overflow of pair m/2 - 1 for even
+    // m, minus the last pair's for m = 0: 2^N == -1), zero for odd m
+    const BSlot b = bp_slot(smem, 0, l);
+    short *hx = (short *)(smem + bp_slot_bytes(l));   // after the slot: HP pair overflows
+#pragma unroll
+    for (int r = 0; r < PP; ++r) {
+        const int pp = t + RP_NT * r;
+        *(rp_v4u *)(b.f + 2 * pp) = pr_words(x[0][r]);
+        hx[pp] = (short)x[0][r].h;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < PP; ++r) {
+        const int pp = t + RP_NT * r;
+        const int hv = hx[pp ? pp - 1 : HP - 1];
+        *(short *)(b.c + 2 * pp) = (short)((pp ? hv : -hv) & 0xff);   // c_2pp = hin (|hin| < 128), c_2pp+1 = 0
+    }
+    __syncthreads();
+    if (t < 64) {
+        const int tv = bp_canon(b, l, t);
+        if (t == 0) SL[1] = (u32)tv;
+    }
+    __syncthreads();
+    const long sl = blockIdx.x;
+    u64 *dst = dig + (size_t)sl * l;
+#pragma unroll
+    for (int r = 0; r < PP; ++r) {
+        const int pp = t + RP_NT * r;
+        *(rp_v4u *)(dst + 2 * pp) = *(const rp_v4u *)(b.f + 2 * pp);
+    }
+    for (int w = t; w < cbw; w += RP_NT) cb[(size_t)sl * cbw + w] = 0;
+    if (t == 0) top[sl] = (int)SL[1];
 }

@@ -51,3 +51,18 @@ rp_pair_fn rp_pair_get(int l, int op)
     }
     return nullptr;
 }
+
+void (*rp_scale_get_p1())(u64 *, u64 *, int *, u32, u32) { return k_rscale<1>; }
+
+void (*rp_scale_get_p2())(u64 *, u64 *, int *, u32, u32);
+void (*rp_scale_get_p4())(u64 *, u64 *, int *, u32, u32);
+
+rp_scale_fn rp_scale_get(int l)
+{
+    switch (l) {
+    case 1024: return rp_scale_get_p1();
+    case 2048: return rp_scale_get_p2();
+    case 4096: return rp_scale_get_p4();
+    }
+    return nullptr;
+}

@@ -25,3 +25,5 @@ rp_pair_fn rp_pair_get_p4(int op)
                                       k_rpair<4, OP_FIX>, k_rpair<4, OP_TWOXMY>, k_rpair<4, OP_IBFLY>};
     return op >= 0 && op < 6 ? tab[op] : nullptr;
 }
+
+void (*rp_scale_get_p4())(u64 *, u64 *, int *, u32, u32) { return k_rscale<4>; }
