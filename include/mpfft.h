@@ -80,6 +80,22 @@ int mpfft_check_params(long n1, long n2, unsigned long depth, unsigned long w);
  * (mul_fft.c:3193-3203). */
 int mpfft_plan_info(long n1, long n2, unsigned long depth, unsigned long w, long *out);
 
+/* ---- sqrt2 front end: replaces new_mpn_mul6, mul_fft.c:3573-3668 ----------------------
+ * A length-4n convolution mod 2^N + 1 (N = 2^depth w) through the 4n-th root of unity
+ * sqrt2^w, sqrt2 = 2^(3N/4) - 2^(N/4): twice the transform length of new_mpn_mul at the
+ * same coefficient size, bits1 = (N - depth - 1)/2 (:3578).  Any w with 64 | N (odd w is
+ * where sqrt2 matters).  The reference needs trunc > 2n; here smaller products also work. */
+void new_mpn_mul6(mp_limb_t *r1, mp_limb_t *i1, mp_size_t n1, mp_limb_t *i2, mp_size_t n2,
+                  mp_bitcnt_t depth, mp_bitcnt_t w);
+int mpfft_mul6_ex(uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i2, long n2,
+                  unsigned long depth, unsigned long w);
+int mpfft_mul6_device(uint64_t *d_r, const uint64_t *d_i1, long n1, const uint64_t *d_i2, long n2,
+                      unsigned long depth, unsigned long w, void *d_ws, size_t ws_bytes, void *stream);
+size_t mpfft_workspace_bytes6(long n1, long n2, unsigned long depth, unsigned long w);
+int mpfft_check_params6(long n1, long n2, unsigned long depth, unsigned long w);
+/* out[10] as mpfft_plan_info, for new_mpn_mul6 (mul_fft.c:3575-3603) */
+int mpfft_plan_info6(long n1, long n2, unsigned long depth, unsigned long w, long *out);
+
 /* Byte offsets inside a single-GPU workspace (tests / multi-GPU driver):
  * out[8] = digA, topA, cbA, digB, topB, cbB, slots per operand, carry-mask words per slot. */
 int mpfft_workspace_layout(long n1, long n2, unsigned long depth, unsigned long w, size_t *out);

@@ -103,6 +103,18 @@ def lib():
         h.mpfft_choose.restype = ctypes.c_int
         h.mpfft_mul_auto.argtypes = [_u64p, _u64p, _L, _u64p, _L]
         h.mpfft_mul_auto.restype = ctypes.c_int
+        h.new_mpn_mul6.argtypes = [_u64p, _u64p, _L, _u64p, _L, _UL, _UL]
+        h.new_mpn_mul6.restype = None
+        h.mpfft_mul6_ex.argtypes = [_u64p, _u64p, _L, _u64p, _L, _UL, _UL]
+        h.mpfft_mul6_ex.restype = ctypes.c_int
+        h.mpfft_mul6_device.argtypes = [_vp, _vp, _L, _vp, _L, _UL, _UL, _vp, ctypes.c_size_t, _vp]
+        h.mpfft_mul6_device.restype = ctypes.c_int
+        h.mpfft_workspace_bytes6.argtypes = [_L, _L, _UL, _UL]
+        h.mpfft_workspace_bytes6.restype = ctypes.c_size_t
+        h.mpfft_check_params6.argtypes = [_L, _L, _UL, _UL]
+        h.mpfft_check_params6.restype = ctypes.c_int
+        h.mpfft_plan_info6.argtypes = [_L, _L, _UL, _UL, ctypes.POINTER(ctypes.c_long)]
+        h.mpfft_plan_info6.restype = ctypes.c_int
         _lib = h
     return _lib
 
@@ -172,6 +184,61 @@ def mul_auto(i1, i2):
     if rc:
         raise MpfftError(rc, f"mul_auto(n1={len(i1)}, n2={len(i2)})")
     return r
+
+
+# ---- the sqrt2 front end (new_mpn_mul6, mul_fft.c:3573-3668) --------------------------
+
+def check_params6(n1, n2, depth, w):
+    return lib().mpfft_check_params6(n1, n2, depth, w)
+
+
+def plan_info6(n1, n2, depth, w):
+    """derived parameters of new_mpn_mul6 (mul_fft.c:3575-3603): bits1 = (N - depth - 1)/2,
+    trunc over a length-4n convolution"""
+    out = (ctypes.c_long * 10)()
+    rc = lib().mpfft_plan_info6(n1, n2, depth, w, out)
+    if rc:
+        raise MpfftError(rc, f"plan6(n1={n1}, n2={n2}, depth={depth}, w={w})")
+    keys = ("n", "l", "NC", "j1", "j2", "trunc", "bits1", "NR", "tpb", "U")
+    return dict(zip(keys, list(out)))
+
+
+def workspace_bytes6(n1, n2, depth, w):
+    return int(lib().mpfft_workspace_bytes6(n1, n2, depth, w))
+
+
+def new_mpn_mul6(r1, i1, n1, i2, n2, depth, w):
+    """Reference-shaped entry (mul_fft.c:3573): r1[:n1+n2] = i1[:n1] * i2[:n2] through the
+    sqrt2 transforms (length 4n, root sqrt2^w)"""
+    if len(r1) < n1 + n2 or len(i1) < n1 or len(i2) < n2:
+        raise ValueError("buffer shorter than the stated limb count")
+    rc = lib().mpfft_mul6_ex(_p(r1), _p(i1), n1, _p(i2), n2, depth, w)
+    if rc:
+        raise MpfftError(rc, f"new_mpn_mul6(n1={n1}, n2={n2}, depth={depth}, w={w})")
+
+
+def mul6(i1, i2, depth, w):
+    i1 = np.ascontiguousarray(i1, dtype=np.uint64)
+    i2 = np.ascontiguousarray(i2, dtype=np.uint64)
+    r = np.zeros(len(i1) + len(i2), dtype=np.uint64)
+    new_mpn_mul6(r, i1, len(i1), i2, len(i2), depth, w)
+    return r
+
+
+def alloc_workspace6(n1, n2, depth, w, device="cuda"):
+    import torch
+    nb = workspace_bytes6(n1, n2, depth, w)
+    if nb == 0:
+        raise MpfftError(check_params6(n1, n2, depth, w), "workspace6")
+    return torch.empty(nb, dtype=torch.uint8, device=device)
+
+
+def mul6_device(d_r, d_i1, n1, d_i2, n2, depth, w, ws, stream=None):
+    """new_mpn_mul6 on HBM-resident operands; queued on `stream`, not synchronised."""
+    rc = lib().mpfft_mul6_device(_ptr(d_r), _ptr(d_i1), n1, _ptr(d_i2), n2, depth, w, _ptr(ws),
+                                 ws.numel() * ws.element_size(), _stream(stream))
+    if rc:
+        raise MpfftError(rc, "mpfft_mul6_device")
 
 
 def fill_random(count, seed):

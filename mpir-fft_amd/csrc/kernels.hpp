@@ -355,6 +355,119 @@ __global__ __launch_bounds__(1024) void k_pairop(PairArgs a)
 }
 
 // --------------------------------------------------------------------------
+// the sqrt2 front end's top level (new_mpn_mul6, mul_fft.c:3573-3668): the 4n-point
+// transform pairs slot k (first half) with slot 2n + k (second half) through the 4n-th
+// root of unity z = sqrt2^w (z^2 = 2^w), sqrt2 = 2^(3N/4) - 2^(N/4) mod 2^N + 1.
+//   S2_FWD   split coefficients k, k + 2n of the operand (fused FFT_split_bits), then
+//            (a, b) -> (a + b, z^k (a - b))       FFT_radix2_mfa_truncate_sqrt2 :2232-2281
+//   S2_FILL  second half slot u <- z^u * first half slot u for the rows past trunc2
+//            (the inputs known to be zero upstream)  IFFT_radix2_mfa_truncate_sqrt2 :2682-2692
+//   S2_IBFLY (a, b) -> (a + z^-k b, a - z^-k b) for k < trunc - 2n, else a <- 2a  :2698-2740
+// --------------------------------------------------------------------------
+enum { S2_FWD = 0, S2_FILL = 1, S2_IBFLY = 2 };
+
+struct S2Args {
+    u64 *dig[2];
+    u64 *cb[2];
+    int *top[2];
+    const u64 *src[2];   // S2_FWD: the operands
+    long nsrc[2];
+    u64 bits1;
+    u64 N;
+    u64 w;
+    int l;
+    int op;
+    long half;           // 2n: slot offset of the second half
+    long k0;             // first k of the launch (S2_FILL: trunc2 NC)
+    long tlo;            // S2_IBFLY: pairs k < tlo, doubling above; S2_FWD: 0 = second half unused
+};
+
+// x[1] <- z^m x[1] (x[2] scratch): m w even: 2^(m w / 2); odd: 2^((m w - 1)/2) sqrt2 (FFT_twiddle_sqrt2 :972)
+template <int U>
+__device__ __forceinline__ void s2_root(const WG &c, i64 (&x)[3][2 * U], u64 m, u64 w, u64 N, int l, i64 *stage, int rb)
+{
+    const u64 N2 = 2 * N, mw = m * w;
+    u64 ee[3] = {0, 0, 0};
+    if (!(mw & 1)) {
+        ee[1] = (mw / 2) % N2;
+        rotate_set<U, 3>(c, x, ee, N, l, stage, rb);
+        return;
+    }
+    const u64 e = (mw - 1) / 2;
+#pragma unroll
+    for (int q = 0; q < 2 * U; ++q) x[2][q] = x[1][q];
+    ee[1] = (e + 3 * N / 4) % N2;
+    ee[2] = (e + N / 4) % N2;
+    rotate_set<U, 3>(c, x, ee, N, l, stage, rb);
+#pragma unroll
+    for (int q = 0; q < 2 * U; ++q) {
+        x[1][q] -= x[2][q];
+        x[2][q] = 0;
+    }
+}
+
+__host__ __device__ constexpr int s2_rb(int U) { return U == 1 ? 3 : 1; }
+
+template <int U>
+__global__ __launch_bounds__(1024) void k_s2op(S2Args a)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const WG c = wg_ctx();
+    const int l = a.l;
+    constexpr int RB = s2_rb(U);
+    const Lds sm = lds_carve<U, 3>(smem, l, RB, c.nw);
+    const int op = blockIdx.y;
+    Coef st;
+    st.dig = a.dig[op];
+    st.cb = a.cb[op];
+    st.top = a.top[op];
+    const long k = a.k0 + (long)blockIdx.x;
+    long slot[3] = {k, a.half + k, k};
+    bool keep[3] = {true, true, false};
+    i64 x[3][2 * U];
+    zero_coeff<U>(x[2]);
+    if (a.op == S2_FWD) {
+        const SrcSlice whole{0, 1, 0};
+        load_split<U>(c, x[0], a.src[op], a.nsrc[op], whole, k, a.bits1, l);
+        load_split<U>(c, x[1], a.src[op], a.nsrc[op], whole, a.half + k, a.bits1, l);
+#pragma unroll
+        for (int q = 0; q < 2 * U; ++q) {
+            const i64 s = x[0][q] + x[1][q], d = x[0][q] - x[1][q];
+            x[0][q] = s;
+            x[1][q] = d;
+        }
+        if (a.tlo) s2_root<U>(c, x, (u64)k, a.w, a.N, l, sm.stage, RB);
+        else keep[1] = false;
+    } else if (a.op == S2_FILL) {
+        load_coeff<U>(c, x[0], st, slot[0], l);
+#pragma unroll
+        for (int q = 0; q < 2 * U; ++q) x[1][q] = x[0][q];
+        s2_root<U>(c, x, (u64)k, a.w, a.N, l, sm.stage, RB);
+        keep[0] = false;
+    } else {
+        load_coeff<U>(c, x[0], st, slot[0], l);
+        if (k < a.tlo) {
+            load_coeff<U>(c, x[1], st, slot[1], l);
+            s2_root<U>(c, x, (u64)(2 * a.half - k), a.w, a.N, l, sm.stage, RB);   // z^-k = z^(4n-k)
+#pragma unroll
+            for (int q = 0; q < 2 * U; ++q) {
+                const i64 s = x[0][q] + x[1][q], d = x[0][q] - x[1][q];
+                x[0][q] = s;
+                x[1][q] = d;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 2 * U; ++q) {
+                x[0][q] *= 2;
+                x[1][q] = 0;
+            }
+            keep[1] = false;
+        }
+    }
+    normalize_store<U, 3>(c, x, slot, keep, false, st, l, sm);
+}
+
+// --------------------------------------------------------------------------
 // scaling by 2^-(depth+1) and canonicalisation (mul_fft.c:3256-3260)
 // --------------------------------------------------------------------------
 template <int U>

@@ -66,6 +66,7 @@ struct Plan {
     bool lds;           // LDS-resident radix-2^5 passes (lkernels.hpp)
     bool big;           // LDS-resident passes for 512 <= l <= 4096 (bkernels.hpp)
     bool rpass;         // register-resident passes (rkernels.hpp) where they apply, l = 1024, 2048, 4096
+    bool sqrt2;         // new_mpn_mul6 plan: 4n slots, bits1 = (N - depth - 1)/2, Tr up to 2 NR
     size_t slots;       // allocated slots per operand
     size_t off_digA, off_topA, off_cbA, off_digB, off_topB, off_cbB, off_lo, off_hi, off_bg, off_bp, off_bc, bytes;
     long nblk;
@@ -75,9 +76,12 @@ static int ilog2(long v) { int d = 0; while ((1L << d) < v) ++d; return d; }
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned long w)
+// sqrt2: the new_mpn_mul6 front end (mul_fft.c:3573-3603): a length-4n convolution with
+// bits1 = (N - (depth + 1))/2 (:3578) and the same trunc rule (:3603)
+static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned long w, bool sqrt2 = false)
 {
     memset(p, 0, sizeof(*p));
+    p->sqrt2 = sqrt2;
     if (n1 < 1 || n2 < 1) return MPFFT_EINVAL;
     if (depth < 2 || depth > 30 || w < 1 || w > 4096) return MPFFT_EINVAL;
     p->n1 = n1;
@@ -89,7 +93,8 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
     p->N = (u64)p->n * w;
     p->l = (long)(p->N / 64);
     if (p->N <= depth) return MPFFT_EINVAL;
-    p->bits1 = (p->N - depth) / 2;
+    if (sqrt2 && p->N <= depth + 1) return MPFFT_EINVAL;
+    p->bits1 = (p->N - depth - (sqrt2 ? 1 : 0)) / 2;
     if (p->bits1 < 1) return MPFFT_EINVAL;
     p->NC = 1L << (depth / 2);
     p->NR = 2 * p->n / p->NC;
@@ -98,7 +103,7 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
     p->j1 = (long)((64 * (u64)n1 - 1) / p->bits1 + 1);
     p->j2 = (long)((64 * (u64)n2 - 1) / p->bits1 + 1);
     p->len = p->j1 + p->j2 - 1;
-    if (p->len > 2 * p->n) return MPFFT_ETOOBIG;             // product does not fit the convolution
+    if (p->len > (sqrt2 ? 4 : 2) * p->n) return MPFFT_ETOOBIG;   // product does not fit the convolution
     p->trunc = ((p->j1 + p->j2 - 2 + 2 * p->NC) / (2 * p->NC)) * 2 * p->NC;
     p->Tr = p->trunc / p->NC;
     p->total = n1 + n2;
@@ -121,7 +126,7 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
         p->maxlogg = wv_fns(p->wU, p->wfull).maxlogg;
         const char *e = getenv("MPFFT_WLOGG");
         if (e && atoi(e) >= 1 && atoi(e) <= p->maxlogg) p->maxlogg = atoi(e);
-        p->fuse_scale = p->Tr == p->NR;
+        p->fuse_scale = p->Tr == p->NR && !sqrt2;
         const char *el = getenv("MPFFT_LDS");
         p->lds = !(el && !strcmp(el, "0"));
         if (p->lds) {
@@ -150,7 +155,7 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
             p->maxlogg = p->maxlogg_c = rl;
         }
     }
-    p->slots = (size_t)2 * p->n;
+    p->slots = (size_t)(sqrt2 ? 4 : 2) * p->n;
     size_t o = 0;
     const size_t dig = p->slots * p->l * 8, top = align_up(p->slots * 4, 256);
     const size_t cbb = align_up(p->slots * cb_words((int)p->l) * 8, 256);
@@ -248,6 +253,7 @@ struct Exec {
     long src_chunk = 0;      // operands are column slices (mpfft_shard.src_chunk), 0 = whole operands
     u32 *zflags = nullptr;   // non-null: the first forward column pass clears the combine's look-back flags
     long zflags_n = 0;       // (u32 words), so combine_single needs no separate fill launch
+    int in_rows = 0;         // non-zero: inputs live in column rows [0, in_rows) (default: the trunc rows)
 
     Exec(const Plan &p, hipStream_t st) : P(p), s(st) { nw = P.tpb / 64; }
 
@@ -281,6 +287,18 @@ struct Exec {
         ccb = (int)P.NC;
         cbb = P.lbC;
         cbs = (long)P.Tr * P.NC;
+    }
+
+    // both layouts start `slots` slots further on (the sqrt2 plan's second half)
+    void shift(long slots)
+    {
+        const long cbw = cb_words((int)P.l);
+        for (int k = 0; k < 2; ++k) {
+            col.dig[k] += slots * P.l;
+            col.cb[k] += slots * cbw;
+            col.top[k] += slots;
+        }
+        row = col;
     }
 
     // rotation staging buffers for a G-coefficient pass: as many as fit in 64 KiB
@@ -477,7 +495,7 @@ struct Exec {
                 a.src[0] = srcA; a.nsrc[0] = nA;
                 a.src[1] = srcB; a.nsrc[1] = nB;
                 a.src_chunk = src_chunk;
-                a.zero_from = (int)P.Tr;
+                a.zero_from = in_rows ? in_rows : (int)P.Tr;
                 a.zp = zflags;
                 a.zn = zflags_n;
             } else {
@@ -886,8 +904,87 @@ static void prof_mark(int call, int stage, hipStream_t s)
     (void)hipEventRecord(g_prof.ev[call * (MPFFT_NSTAGES + 1) + stage], s);
 }
 
+// the sqrt2 top level (kernels.hpp k_s2op): one workgroup per k in [k0, k0 + cnt)
+static int s2_launch(const Plan &P, const Exec &X, int op, const u64 *srcA, const u64 *srcB, long k0, long cnt,
+                     long tlo, int nops)
+{
+    if (cnt <= 0) return MPFFT_OK;
+    S2Args a;
+    memset(&a, 0, sizeof(a));
+    for (int k = 0; k < 2; ++k) {
+        a.dig[k] = X.col.dig[k];
+        a.cb[k] = X.col.cb[k];
+        a.top[k] = X.col.top[k];
+    }
+    a.src[0] = srcA; a.nsrc[0] = P.n1;
+    a.src[1] = srcB; a.nsrc[1] = P.n2;
+    a.bits1 = P.bits1;
+    a.N = P.N;
+    a.w = (u64)P.w;
+    a.l = (int)P.l;
+    a.op = op;
+    a.half = 2 * P.n;
+    a.k0 = k0;
+    a.tlo = tlo;
+    void (*f)(S2Args) = nullptr;
+    switch (P.U) {
+    case 1: f = k_s2op<1>; break;
+    case 2: f = k_s2op<2>; break;
+    case 4: f = k_s2op<4>; break;
+    }
+    if (!f) return MPFFT_EUNSUPPORTED;
+    const size_t lds = lds_bytes((int)P.l, s2_rb(P.U), 3, P.U, X.nw);
+    allow_lds((const void *)f, lds);
+    hipLaunchKernelGGL(f, dim3((unsigned)cnt, (unsigned)nops), dim3(P.tpb), lds, X.s, a);
+    HIPCHK(hipGetLastError());
+    return MPFFT_OK;
+}
+
+// new_mpn_mul6 (mul_fft.c:3573-3668) on the GPU: the sqrt2 top level (k_s2op) around two
+// length-2n MFA multiplies that reuse every stage of run_all -- the first half full, the
+// second truncated to trunc2 = Tr - NR rows (FFT/IFFT_radix2_mfa_truncate_sqrt2 :2212, :2593)
+static int run_all6(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, unsigned char *ws, hipStream_t s)
+{
+    Plan P1 = P, P2 = P, PS = P;
+    P1.Tr = P.NR;
+    P1.trunc = 2 * P.n;
+    P2.Tr = P.Tr > P.NR ? P.Tr - P.NR : 0;
+    P2.trunc = P2.Tr * P.NC;
+    PS.depth = P.depth + 1;   // scale by 2^-(depth+2) (:3654-3658)
+    Exec X1(P1, s), X2(P2, s), XS(PS, s), XC(P, s);
+    X1.single(ws);
+    X2.single(ws);
+    X2.shift(2 * P.n);
+    X2.in_rows = (int)P.NR;   // the second half's inputs are all live (FFT_radix2_truncate1_twiddle)
+    XS.single(ws);
+    XC.single(ws);
+    const bool two = P2.Tr > 0;
+    const long tlo = P.trunc - 2 * P.n;   // pairs k < tlo carry both halves
+    int rc;
+    if ((rc = s2_launch(P, X1, S2_FWD, d_i1, d_i2, 0, 2 * P.n, two ? 1 : 0, 2))) return rc;
+    if ((rc = X1.fwd_columns(nullptr, 0, nullptr, 0, 2))) return rc;
+    if ((rc = X1.fwd_rows(2))) return rc;
+    if (two) {
+        if ((rc = X2.fwd_columns(nullptr, 0, nullptr, 0, 2))) return rc;
+        if ((rc = X2.fwd_rows(2))) return rc;
+    }
+    if ((rc = X1.pointwise())) return rc;
+    if (two && (rc = X2.pointwise())) return rc;
+    if ((rc = X1.inv_rows())) return rc;
+    if (two && (rc = X2.inv_rows())) return rc;
+    if ((rc = X1.itft(0, P.NR, P.NR))) return rc;
+    if (two) {
+        if ((rc = s2_launch(P, X1, S2_FILL, nullptr, nullptr, P2.Tr * P.NC, (P.NR - P2.Tr) * P.NC, 0, 1))) return rc;
+        if ((rc = X2.itft1(0, P.NR, P2.Tr))) return rc;
+    }
+    if ((rc = s2_launch(P, X1, S2_IBFLY, nullptr, nullptr, 0, 2 * P.n, tlo > 0 ? tlo : 0, 1))) return rc;
+    if ((rc = XS.scale())) return rc;
+    return XC.combine_single(d_r, ws);
+}
+
 static int run_all(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, unsigned char *ws, hipStream_t s)
 {
+    if (P.sqrt2) return run_all6(P, d_r, d_i1, d_i2, ws, s);
     Exec X(P, s);
     X.single(ws);
     X.zflags = X.comb_flags(ws);
@@ -1172,12 +1269,9 @@ static int ensure_buf(void **p, size_t *have, size_t need)
     return MPFFT_OK;
 }
 
-int mpfft_mul_ex(uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i2, long n2, unsigned long depth,
-                 unsigned long w)
+static int mul_host(const Plan &P, uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i2, long n2)
 {
-    Plan P;
-    int rc = make_plan(&P, n1, n2, depth, w);
-    if (rc) return rc;
+    int rc;
     (void)hipGetLastError();
     int ndev = 0, dev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return MPFFT_ENODEV;
@@ -1195,6 +1289,71 @@ int mpfft_mul_ex(uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i2, 
     HIPCHK(hipMemcpyAsync(r1, d_r, (size_t)(n1 + n2) * 8, hipMemcpyDeviceToHost, C.stream));
     HIPCHK(hipStreamSynchronize(C.stream));
     return MPFFT_OK;
+}
+
+int mpfft_mul_ex(uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i2, long n2, unsigned long depth,
+                 unsigned long w)
+{
+    Plan P;
+    int rc = make_plan(&P, n1, n2, depth, w);
+    if (rc) return rc;
+    return mul_host(P, r1, i1, n1, i2, n2);
+}
+
+// ---- the sqrt2 front end new_mpn_mul6 (mul_fft.c:3573-3668) ---------
+int mpfft_check_params6(long n1, long n2, unsigned long depth, unsigned long w)
+{
+    Plan P;
+    return make_plan(&P, n1, n2, depth, w, true);
+}
+
+size_t mpfft_workspace_bytes6(long n1, long n2, unsigned long depth, unsigned long w)
+{
+    Plan P;
+    if (make_plan(&P, n1, n2, depth, w, true)) return 0;
+    return P.bytes;
+}
+
+int mpfft_plan_info6(long n1, long n2, unsigned long depth, unsigned long w, long *out)
+{
+    Plan P;
+    int rc = make_plan(&P, n1, n2, depth, w, true);
+    if (rc) return rc;
+    out[0] = P.n; out[1] = P.l; out[2] = P.NC; out[3] = P.j1; out[4] = P.j2;
+    out[5] = P.trunc; out[6] = (long)P.bits1; out[7] = P.NR; out[8] = P.tpb; out[9] = P.U;
+    return MPFFT_OK;
+}
+
+int mpfft_mul6_device(uint64_t *d_r, const uint64_t *d_i1, long n1, const uint64_t *d_i2, long n2,
+                      unsigned long depth, unsigned long w, void *d_ws, size_t ws_bytes, void *stream)
+{
+    Plan P;
+    int rc = make_plan(&P, n1, n2, depth, w, true);
+    if (rc) return rc;
+    if (!d_ws || ws_bytes < P.bytes) return MPFFT_ENOMEM;
+    (void)hipGetLastError();
+    return run_all(P, d_r, d_i1, d_i2, (unsigned char *)d_ws, (hipStream_t)stream);
+}
+
+int mpfft_mul6_ex(uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i2, long n2, unsigned long depth,
+                  unsigned long w)
+{
+    Plan P;
+    int rc = make_plan(&P, n1, n2, depth, w, true);
+    if (rc) return rc;
+    return mul_host(P, r1, i1, n1, i2, n2);
+}
+
+// mul_fft.c:3573 -- same signature and meaning; fails loudly instead of segfaulting
+void new_mpn_mul6(mp_limb_t *r1, mp_limb_t *i1, mp_size_t n1, mp_limb_t *i2, mp_size_t n2, mp_bitcnt_t depth,
+                  mp_bitcnt_t w)
+{
+    int rc = mpfft_mul6_ex(r1, i1, n1, i2, n2, depth, w);
+    if (rc) {
+        fprintf(stderr, "new_mpn_mul6(n1=%ld, n2=%ld, depth=%lu, w=%lu): %s\n", (long)n1, (long)n2,
+                (unsigned long)depth, (unsigned long)w, mpfft_strerror(rc));
+        abort();
+    }
 }
 
 // release the calling device's cached workspace (the next call re-allocates)

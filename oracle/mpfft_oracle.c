@@ -685,6 +685,202 @@ void orc_new_mpn_mul(limb_t *r1, const limb_t *i1, long n1, const limb_t *i2, lo
 }
 
 /* ------------------------------------------------------------------------- */
+/* L6: the sqrt2 front end new_mpn_mul6 (mul_fft.c:3573-3668)                */
+/* ------------------------------------------------------------------------- */
+
+/* r = a * z^i mod p, z the 4n-th root of unity sqrt2^w (z^2 = 2^w), N = n w.
+ * i w even: the shift 2^(i w / 2) (FFT_twiddle, mul_fft.c:926, called with (i/2, n, w)
+ * for odd w and with (i, 2n, w/2) for even w); i w odd: 2^((i w - 1)/2) sqrt2 with
+ * sqrt2 = 2^(3N/4) - 2^(N/4) (FFT_twiddle_sqrt2 :972 / FFT_radix2_butterfly_sqrt2 :591:
+ * "multiply by 2^(j + wn/4 + ik), then again by a further 2^(wn/2) and subtract").
+ * r must not alias a; t is scratch of l + 1 limbs. */
+static void o_mul_root4n(limb_t *r, const limb_t *a, long l, unsigned long i, unsigned long w, limb_t *t)
+{
+    unsigned long N = 64UL * (unsigned long)l, iw = i * w;
+    if ((iw & 1) == 0) {
+        o_mul_2exp(r, a, l, iw / 2);
+        return;
+    }
+    unsigned long e = (iw - 1) / 2;
+    o_mul_2exp(t, a, l, e + 3 * N / 4);
+    o_mul_2exp(r, a, l, e + N / 4);
+    o_sub_n(r, t, r, l + 1);
+}
+
+/* mul_fft.c:2212-2355 FFT_radix2_mfa_truncate_sqrt2: length-4n truncated transform
+ * with root z.  Top level pairs (j, j + 2n) by sum / z^j difference (:2232-2281), then
+ * the first half is a full length-2n MFA (:2283-2316) and the second a truncated one
+ * over trunc2 = (trunc - 2n)/n1 rows (:2318-2354).  trunc <= 2n (the reference needs
+ * trunc > 2n; it indexes ii with trunc2 < 0) leaves the second half unused. */
+static void o_fft_mfa_trunc_sqrt2(octx *c, limb_t **ii, long n, unsigned long w, long n1, long trunc)
+{
+    long l = c->l, n2 = 2 * n / n1;
+    long trunc2 = trunc > 2 * n ? (trunc - 2 * n) / n1 : 0;
+    unsigned dr = o_log2(n2), dc = o_log2(n1);
+    for (long col = 0; col < n1; col++) {
+        long j = col;
+        for (; j < trunc - 2 * n; j += n1) {          /* (a, b) -> (a + b, z^j (a - b)) */
+            o_add_n(c->t1, ii[j], ii[2 * n + j], l + 1);
+            o_sub_n(c->t3, ii[j], ii[2 * n + j], l + 1);
+            o_mul_root4n(c->t2, c->t3, l, (unsigned long)j, w, ii[2 * n + j]);
+            SWAP_PTR(ii[j], c->t1);
+            SWAP_PTR(ii[2 * n + j], c->t2);
+        }
+        if (trunc2)
+            for (; j < 2 * n; j += n1)                /* b = 0: z^j a */
+                o_mul_root4n(ii[2 * n + j], ii[j], l, (unsigned long)j, w, c->t3);
+        o_fft_tw(c, ii + col, n1, n2 / 2, w * (unsigned long)n1, w, 0, col, 1);
+        for (long r = 0; r < n2; r++) {
+            long s = o_revbin(r, dr);
+            if (r < s) SWAP_PTR(ii[col + r * n1], ii[col + s * n1]);
+        }
+    }
+    for (long row = 0; row < n2; row++) {
+        limb_t **rp = ii + row * n1;
+        o_fft(c, rp, 1, n1 / 2, w * (unsigned long)n2);
+        for (long k = 0; k < n1; k++) {
+            long t = o_revbin(k, dc);
+            if (k < t) SWAP_PTR(rp[k], rp[t]);
+        }
+    }
+    ii += 2 * n;
+    if (!trunc2) return;
+    for (long col = 0; col < n1; col++) {
+        o_fft_trunc1_tw(c, ii + col, n1, n2 / 2, w * (unsigned long)n1, w, 0, col, 1, trunc2);
+        for (long r = 0; r < n2; r++) {
+            long s = o_revbin(r, dr);
+            if (r < s) SWAP_PTR(ii[col + r * n1], ii[col + s * n1]);
+        }
+    }
+    for (long s = 0; s < trunc2; s++) {
+        limb_t **rp = ii + o_revbin(s, dr) * n1;
+        o_fft(c, rp, 1, n1 / 2, w * (unsigned long)n2);
+        for (long k = 0; k < n1; k++) {
+            long t = o_revbin(k, dc);
+            if (k < t) SWAP_PTR(rp[k], rp[t]);
+        }
+    }
+}
+
+/* mul_fft.c:2593-2743 IFFT_radix2_mfa_truncate_sqrt2: result x 4n for slots < trunc */
+static void o_ifft_mfa_trunc_sqrt2(octx *c, limb_t **ii, long n, unsigned long w, long n1, long trunc)
+{
+    long l = c->l, n2 = 2 * n / n1;
+    long trunc2 = trunc > 2 * n ? (trunc - 2 * n) / n1 : 0;
+    unsigned dr = o_log2(n2), dc = o_log2(n1);
+    for (long row = 0; row < n2; row++) {             /* first half: full inverse */
+        limb_t **rp = ii + row * n1;
+        for (long k = 0; k < n1; k++) {
+            long t = o_revbin(k, dc);
+            if (k < t) SWAP_PTR(rp[k], rp[t]);
+        }
+        o_ifft(c, rp, 1, n1 / 2, w * (unsigned long)n2);
+    }
+    for (long col = 0; col < n1; col++) {
+        for (long r = 0; r < n2; r++) {
+            long s = o_revbin(r, dr);
+            if (r < s) SWAP_PTR(ii[col + r * n1], ii[col + s * n1]);
+        }
+        o_ifft_tw(c, ii + col, n1, n2 / 2, w * (unsigned long)n1, w, 0, col, 1);
+    }
+    limb_t **jj = ii + 2 * n;
+    for (long s = 0; s < trunc2; s++) {               /* second half: computed rows */
+        limb_t **rp = jj + o_revbin(s, dr) * n1;
+        for (long k = 0; k < n1; k++) {
+            long t = o_revbin(k, dc);
+            if (k < t) SWAP_PTR(rp[k], rp[t]);
+        }
+        o_ifft(c, rp, 1, n1 / 2, w * (unsigned long)n2);
+    }
+    for (long col = 0; col < n1; col++) {
+        if (trunc2) {
+            for (long r = 0; r < trunc2; r++) {
+                long s = o_revbin(r, dr);
+                if (r < s) SWAP_PTR(jj[col + r * n1], jj[col + s * n1]);
+            }
+            for (long r = trunc2; r < n2; r++) {      /* x_(u+2n) = 0: z^u (2n x_u) */
+                long u = col + r * n1;
+                o_mul_root4n(jj[u], ii[u], l, (unsigned long)u, w, c->t3);
+            }
+            o_ifft_trunc1_tw(c, jj + col, n1, n2 / 2, w * (unsigned long)n1, w, 0, col, 1, trunc2);
+        }
+        long j = col;
+        for (; j < trunc - 2 * n; j += n1) {          /* (a, b) -> a +- z^-j b */
+            o_mul_root4n(c->t3, jj[j], l, (unsigned long)(4 * n - j), w, c->t1);
+            o_add_n(c->t1, ii[j], c->t3, l + 1);
+            o_sub_n(c->t2, ii[j], c->t3, l + 1);
+            SWAP_PTR(ii[j], c->t1);
+            SWAP_PTR(jj[j], c->t2);
+        }
+        for (; j < 2 * n; j += n1) o_add_n(ii[j], ii[j], ii[j], l + 1);
+    }
+}
+
+static void o_params6(oparams *p, long n1, long n2, unsigned long depth, unsigned long w)
+{
+    o_params(p, n1, n2, depth, w);
+    p->bits1 = ((unsigned long)p->n * w - (depth + 1)) / 2;   /* mul_fft.c:3578 */
+    p->j1 = (long)((64UL * (unsigned long)n1 - 1) / p->bits1 + 1);
+    p->j2 = (long)((64UL * (unsigned long)n2 - 1) / p->bits1 + 1);
+    p->trunc = ((p->j1 + p->j2 - 2 + 2 * p->sqrt_) / (2 * p->sqrt_)) * 2 * p->sqrt_;
+    p->tr = p->trunc / p->sqrt_;
+}
+
+/* mul_fft.c:3573-3668 new_mpn_mul6: length-4n convolution via the sqrt2 transforms,
+ * pointwise over the first half and the computed rows of the second (:3621-3648),
+ * scaling 2^-(depth+2) (:3654-3658) */
+void orc_new_mpn_mul6(limb_t *r1, const limb_t *i1, long n1, const limb_t *i2, long n2,
+                      unsigned long depth, unsigned long w)
+{
+    oparams p;
+    o_params6(&p, n1, n2, depth, w);
+    long n = p.n, l = p.l, sq = p.sqrt_, n2r = 2 * n / sq;
+    octx ca, cb;
+    limb_t *ba, *bb;
+    limb_t **ii = o_table(4 * n, l, &ba, &ca);
+    limb_t **jj = o_table(4 * n, l, &bb, &cb);
+    limb_t *tt = (limb_t *)malloc((size_t)(2 * (l + 1)) * sizeof(limb_t));
+
+    o_split_bits(ii, i1, n1, p.bits1, l);              /* the rest of the table is zero (calloc) */
+    o_fft_mfa_trunc_sqrt2(&ca, ii, n, w, sq, p.trunc);
+    o_split_bits(jj, i2, n2, p.bits1, l);
+    o_fft_mfa_trunc_sqrt2(&cb, jj, n, w, sq, p.trunc);
+
+    long trunc2 = p.trunc > 2 * n ? (p.trunc - 2 * n) / sq : 0;
+    unsigned rw = o_log2(n2r);
+    for (long k = 0; k < 4 * n; k++) {
+        if (k >= 2 * n) {
+            long s = (k - 2 * n) / sq;                 /* row of the second half */
+            if (o_revbin(s, rw) >= trunc2) continue;   /* s = revbin(s'), s' < trunc2 computed */
+        }
+        o_normmod(ii[k], l);
+        o_normmod(jj[k], l);
+        int flag = (int)(ii[k][l] + 2 * jj[k][l]);
+        ii[k][l] = o_mulmod_2expp1(ii[k], ii[k], jj[k], flag, l, tt);
+    }
+
+    o_ifft_mfa_trunc_sqrt2(&ca, ii, n, w, sq, p.trunc);
+    for (long j = 0; j < p.trunc; j++) {
+        o_div_2expmod(ii[j], ii[j], l, (unsigned)(depth + 2));
+        o_normmod(ii[j], l);
+    }
+    memset(r1, 0, (size_t)(n1 + n2) * sizeof(limb_t));
+    o_combine_bits(r1, ii, p.j1 + p.j2 - 1, p.bits1, l, n1 + n2);
+
+    free(tt);
+    free(ii); free(ba);
+    free(jj); free(bb);
+}
+
+void orc_params6(long n1, long n2, unsigned long depth, unsigned long w, long *out)
+{
+    oparams p;
+    o_params6(&p, n1, n2, depth, w);
+    out[0] = p.n; out[1] = p.l; out[2] = p.sqrt_; out[3] = p.j1; out[4] = p.j2;
+    out[5] = p.trunc; out[6] = (long)p.bits1;
+}
+
+/* ------------------------------------------------------------------------- */
 /* ctypes-facing wrappers for the tests (flat arrays of (l+1)-limb blocks)   */
 /* ------------------------------------------------------------------------- */
 

@@ -33,6 +33,8 @@ def lib():
         sig = {
             "orc_new_mpn_mul": [_u64p, _u64p, _L, _u64p, _L, _UL, _UL],
             "orc_params": [_L, _L, _UL, _UL, ctypes.POINTER(ctypes.c_long)],
+            "orc_new_mpn_mul6": [_u64p, _u64p, _L, _u64p, _L, _UL, _UL],
+            "orc_params6": [_L, _L, _UL, _UL, ctypes.POINTER(ctypes.c_long)],
             "orc_normmod": [_u64p, _L],
             "orc_mul_2expmod": [_u64p, _u64p, _L, ctypes.c_uint],
             "orc_div_2expmod": [_u64p, _u64p, _L, ctypes.c_uint],
@@ -73,6 +75,22 @@ def new_mpn_mul(i1, i2, depth, w):
     i2 = np.ascontiguousarray(i2, dtype=np.uint64)
     r = np.zeros(len(i1) + len(i2), dtype=np.uint64)
     lib().orc_new_mpn_mul(_p(r), _p(i1), len(i1), _p(i2), len(i2), depth, w)
+    return r
+
+
+def params6(n1, n2, depth, w):
+    """(n, l, sqrt, j1, j2, trunc, bits1) exactly as new_mpn_mul6 (mul_fft.c:3575-3603)."""
+    out = (ctypes.c_long * 7)()
+    lib().orc_params6(n1, n2, depth, w, out)
+    return tuple(out)
+
+
+def new_mpn_mul6(i1, i2, depth, w):
+    """sqrt2 front end (mul_fft.c:3573-3668): length-4n convolution mod 2^(2^depth w) + 1."""
+    i1 = np.ascontiguousarray(i1, dtype=np.uint64)
+    i2 = np.ascontiguousarray(i2, dtype=np.uint64)
+    r = np.zeros(len(i1) + len(i2), dtype=np.uint64)
+    lib().orc_new_mpn_mul6(_p(r), _p(i1), len(i1), _p(i2), len(i2), depth, w)
     return r
 
 

@@ -89,3 +89,27 @@ def test_chooser_picks_valid_parameters(mp):
             assert mp.check_params(n1, n2, d, w) == 0, (n1, n2, d, w)
     with pytest.raises(mp.MpfftError):
         mp.choose(10**12, 10**12)                       # beyond 4096-limb coefficients at depth 24
+
+
+def test_plan6_matches_reference_parameters(mp, oracle):
+    """new_mpn_mul6's derived parameters (mul_fft.c:3575-3603) equal the oracle's"""
+    from helpers import valid_shape6
+    rng = random.Random(4)
+    checked = 0
+    for _ in range(400):
+        depth = rng.randint(2, 17)
+        w = rng.choice([1, 2, 3, 4, 5, 8, 16, 64])
+        n1, n2 = rng.randint(1, 9000), rng.randint(1, 9000)
+        ok = ((1 << depth) * w) % 64 == 0 and valid_shape6(depth, w, n1, n2) and (1 << depth) * w // 64 <= 4096
+        rc = mp.check_params6(n1, n2, depth, w)
+        assert (rc == 0) == ok, (depth, w, n1, n2, rc)
+        if ok:
+            P = mp.plan_info6(n1, n2, depth, w)
+            n, l, sq, j1, j2, trunc, bits1 = oracle.params6(n1, n2, depth, w)
+            assert (P["n"], P["l"], P["NC"], P["j1"], P["j2"], P["trunc"], P["bits1"]) == \
+                (n, l, sq, j1, j2, trunc, bits1)
+            assert mp.workspace_bytes6(n1, n2, depth, w) > mp.workspace_bytes(1, 1, depth, w)
+            checked += 1
+    assert checked > 50
+    with pytest.raises(mp.MpfftError):
+        mp.mul6(np.ones(4, np.uint64), np.ones(4, np.uint64), 6, 1)   # no GPU here: fails loudly

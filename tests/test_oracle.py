@@ -313,3 +313,40 @@ def test_oracle_golden_vectors(oracle):
         assert hashlib.sha256(r.tobytes()).hexdigest() == c["sha256"], c["name"]
         if "product_hex" in c:
             assert format(to_int(r), "x") == c["product_hex"]
+
+
+def test_new_mpn_mul6_random(oracle):
+    """sqrt2 front end (mul_fft.c:3573): the oracle's length-4n transforms give the exact
+    product (the reference's own check, test_mul4 :5559, compares with mpn_mul)"""
+    from helpers import shapes6
+    rng = random.Random(21)
+    for depth, w, n1, n2 in shapes6(rng, 3):
+        a = oracle.fill_random(n1, rng.getrandbits(64))
+        b = oracle.fill_random(n2, rng.getrandbits(64))
+        r = oracle.new_mpn_mul6(a, b, depth, w)
+        assert to_int(r) == to_int(a) * to_int(b), (depth, w, n1, n2)
+
+
+def test_new_mpn_mul6_test_mul4_shape(oracle):
+    """test_mul4 (mul_fft.c:5559-5608): depth 14, w 1, n1 = n2 = 3/4 of 2n bits1 bits"""
+    depth, w = 14, 1
+    n = 1 << depth
+    bits1 = (n * w - (depth + 1)) // 2
+    int_limbs = 2 * n * bits1 // 64
+    n1 = n2 = (3 * int_limbs) // 4
+    a = oracle.fill_random(n1, 0x1001)
+    b = oracle.fill_random(n2, 0x2002)
+    r = oracle.new_mpn_mul6(a, b, depth, w)
+    assert (r == oracle.gmp_mul(a, b)).all()
+
+
+def test_new_mpn_mul6_adversarial(oracle):
+    from helpers import max_limbs6
+    for depth, w in ((6, 1), (7, 1), (8, 2)):
+        mx = max_limbs6(depth, w)
+        ones = np.full(mx, 2**64 - 1, dtype=np.uint64)
+        one_bit = np.zeros(mx, np.uint64)
+        one_bit[mx - 1] = 1 << 63
+        for a, b in ((ones, ones), (ones[:1], ones), (one_bit, ones), (np.zeros(mx, np.uint64), ones)):
+            r = oracle.new_mpn_mul6(a, b, depth, w)
+            assert to_int(r) == to_int(a) * to_int(b), (depth, w, len(a), len(b))
