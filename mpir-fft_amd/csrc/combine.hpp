@@ -185,18 +185,19 @@ __global__ __launch_bounds__(256) void k_carry_apply(const u64 *lo64, const u32 
 }
 
 // --------------------------------------------------------------------------
-// k_combine1: the whole single-GPU combine in one launch.  Block b owns output limbs
-// [b CB_LIMBS, (b+1) CB_LIMBS): it sums the coefficient windows of its limbs (coalesced,
+// k_combine1<V>: the whole single-GPU combine in one launch.  Block b owns output limbs
+// [256 V b, 256 V (b+1)): it sums the coefficient windows of its limbs (coalesced,
 // limb m = base + k 256 + t), resolves its carries locally, and gets its carry-in by a
 // decoupled look-back over the blocks before it (flags in `st`, zeroed before the
-// launch; workgroups are dispatched in blockIdx order, so every predecessor is resident or done).
+// launch).  b is a ticket from an atomic counter (st[nblocks]), not blockIdx.x: a block
+// only ever waits on blocks that took a smaller ticket, i.e. that are already running,
+// whatever order the hardware dispatches workgroups in.
 // The flag is the whole message (no data published beside it), so relaxed agent-scope
 // atomics suffice: release/acquire would write back / invalidate the XCD's L2 per block.
 // Block flag: 0 not ready, 1 aggregate generates, 2 aggregate propagates, 3 aggregate
 // kills, 4 / 5 inclusive carry-out 0 / 1.
 // --------------------------------------------------------------------------
-#define CB_V 1
-#define CB_LIMBS (256 * CB_V)
+// limbs per block: 256 V (host: comb_v())
 
 // floor(x / d) for x < 2^52: double quotient, then an exact integer fix-up
 __device__ __forceinline__ long udiv_exact(u64 x, u64 d)
@@ -247,16 +248,19 @@ __device__ __forceinline__ void comb_limb(const CombArgs &a, long m, u64 *lo, u3
     *hi = shi;
 }
 
+template <int CB_V>
 __global__ __launch_bounds__(256) void k_combine1(CombArgs a, u64 *r, u32 *st)
 {
+    constexpr int CB_LIMBS = 256 * CB_V;
     __shared__ u64 L[CB_LIMBS];
     __shared__ u32 H[CB_LIMBS + 1];
     __shared__ u64 scr[64];
-    __shared__ u32 sh_cin;
+    __shared__ u32 sh_cin, sh_b;
     const WG c = wg_ctx();
     const long total = a.mcount;
-        // in-order workgroup dispatch: every block below b is resident or done
-    const long b = blockIdx.x;
+    if (c.t == 0) sh_b = __hip_atomic_fetch_add(&st[gridDim.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const long b = sh_b;   // ticket: every block below b has started
     const long base = b * CB_LIMBS;
     // window sums: lo of limb base + i -> L[i], its carry (hi) -> H[i + 1]
 #pragma unroll

@@ -254,6 +254,8 @@ struct Exec {
     u32 *zflags = nullptr;   // non-null: the first forward column pass clears the combine's look-back flags
     long zflags_n = 0;       // (u32 words), so combine_single needs no separate fill launch
     int in_rows = 0;         // non-zero: inputs live in column rows [0, in_rows) (default: the trunc rows)
+    bool defer_double = false;   // itft's top-level doubling is left to scale() (rows [dbl_lo, dbl_hi): 2^-depth)
+    long dbl_lo = 0, dbl_hi = 0;
 
     Exec(const Plan &p, hipStream_t st) : P(p), s(st) { nw = P.tpb / 64; }
 
@@ -266,7 +268,15 @@ struct Exec {
         return (rem + np - 1) / np;
     }
 
-    long comb_blocks() const { return (P.total + CB_LIMBS - 1) / CB_LIMBS; }
+    // k_combine1 block size: 256 comb_v() limbs (MPFFT_CB_V = 1, 2, 4, 8)
+    static int comb_v()
+    {
+        // C3 sweep (profiles/r02/combine_cbv.txt): V = 1: 1.84 ms, 2: 0.94, 4: 0.51, 8: 0.42, 16: see there
+        static const int v = [] { const char *e = getenv("MPFFT_CB_V"); const int x = e ? atoi(e) : 8;
+                                  return x == 1 || x == 2 || x == 4 || x == 16 ? x : 8; }();
+        return v;
+    }
+    long comb_blocks() const { return (P.total + 256L * comb_v() - 1) / (256L * comb_v()); }
     u32 *comb_flags(unsigned char *ws) const { return (u32 *)(ws + P.off_lo); }
     long comb_flag_words() const { return (comb_blocks() + 4) / 4 * 4; }
 
@@ -740,15 +750,26 @@ struct Exec {
     {
         int rc;
         const long h = m / 2;
+        const bool top = defer_double && off == 0 && m == P.NR;   // its doubling folds into the scaling
         if (t == m) return ifft_block(off, m);
         if (t <= h) {
             if ((rc = itft(off, h, t))) return rc;
+            if (top) {
+                dbl_lo = 0;
+                dbl_hi = t;
+                return MPFFT_OK;
+            }
             return pairop(OP_DOUBLE, off, h, 0, t, 0);
         }
         if ((rc = ifft_block(off, h))) return rc;
         if ((rc = pairop(OP_FILL, off, h, t - h, h - (t - h), rho_blk(m)))) return rc;
         if ((rc = itft1(off + h, h, t - h))) return rc;
         if ((rc = pairop(OP_IBFLY, off, h, 0, t - h, rho_blk(m)))) return rc;
+        if (top) {
+            dbl_lo = t - h;
+            dbl_hi = h;
+            return MPFFT_OK;
+        }
         return pairop(OP_DOUBLE, off, h, t - h, h - (t - h), 0);
     }
 
@@ -769,15 +790,29 @@ struct Exec {
         return pairop(OP_IBFLY, off, h, 0, t - h, rho_blk(m));
     }
 
+    // scaling by 2^-(depth+1); rows [dbl_lo, dbl_hi) by 2^-depth (itft's deferred doubling)
     int scale()
     {
-        const long cnt = (long)P.Tr * ccount;
         if (P.fuse_scale) return MPFFT_OK;   // done by the last inverse column pass
+        const u64 e = 2 * P.N - (u64)(P.depth + 1);
+        if (dbl_hi <= dbl_lo) return scale_rows(0, P.Tr, e);
+        int rc;
+        if ((rc = scale_rows(0, dbl_lo, e))) return rc;
+        if ((rc = scale_rows(dbl_lo, dbl_hi, e + 1))) return rc;
+        return scale_rows(dbl_hi, P.Tr, e);
+    }
+
+    int scale_rows(long r0_, long r1_, u64 e)
+    {
+        const long cnt = (r1_ - r0_) * ccount, s0 = r0_ * ccount;
+        if (cnt <= 0) return MPFFT_OK;
+        u64 *dig = col.dig[0] + s0 * P.l, *cbp = col.cb[0] + s0 * cb_words((int)P.l);
+        int *top = col.top[0] + s0;
         if (P.rpass) {   // register-resident scale + canonicalisation (rkernels.hpp)
             rp_scale_fn f = rp_scale_get((int)P.l);
             if (!f) return MPFFT_EUNSUPPORTED;
-            hipLaunchKernelGGL(f, dim3((unsigned)cnt), dim3(RP_NT), rp_scale_lds((int)P.l), s, col.dig[0], col.cb[0],
-                               col.top[0], (unsigned)P.N, (unsigned)(2 * P.N - (u64)(P.depth + 1)));
+            hipLaunchKernelGGL(f, dim3((unsigned)cnt), dim3(RP_NT), rp_scale_lds((int)P.l), s, dig, cbp, top, (unsigned)P.N,
+                               (unsigned)e);
             HIPCHK(hipGetLastError());
             return MPFFT_OK;
         }
@@ -785,8 +820,8 @@ struct Exec {
             wv_scale_fn f = wv_fns(P.wU, P.wfull).scale;
             const size_t lds = (size_t)WPB * 16 * P.l;
             allow_lds((const void *)f, lds);
-            hipLaunchKernelGGL(f, dim3((unsigned)((cnt + WPB - 1) / WPB)), dim3(64 * WPB), lds, s, col.dig[0],
-                               col.cb[0], col.top[0], (int)P.l, P.N, 2 * P.N - (u64)(P.depth + 1), cnt);
+            hipLaunchKernelGGL(f, dim3((unsigned)((cnt + WPB - 1) / WPB)), dim3(64 * WPB), lds, s, dig, cbp, top,
+                               (int)P.l, P.N, e, cnt);
             HIPCHK(hipGetLastError());
             return MPFFT_OK;
         }
@@ -797,10 +832,8 @@ struct Exec {
         case 2: f = k_scale<2>; break;
         case 4: f = k_scale<4>; break;
         }
-        const u64 e = 2 * P.N - (u64)(P.depth + 1);
         allow_lds((const void *)f, lds);
-        hipLaunchKernelGGL(f, dim3((unsigned)cnt), dim3(P.tpb), lds, s, col.dig[0], col.cb[0], col.top[0],
-                           (int)P.l, P.N, e);
+        hipLaunchKernelGGL(f, dim3((unsigned)cnt), dim3(P.tpb), lds, s, dig, cbp, top, (int)P.l, P.N, e);
         HIPCHK(hipGetLastError());
         return MPFFT_OK;
     }
@@ -878,7 +911,10 @@ struct Exec {
             u32 *st = comb_flags(ws);   // (nb + 1) flags, inside the lo64 scratch of the multi-kernel path
             if (zflags != st)           // not already cleared by the first forward column pass
                 HIPCHK(hipMemsetAsync(st, 0, (size_t)comb_flag_words() * 4, s));   // whole 16-byte words: one fill
-            hipLaunchKernelGGL(k_combine1, dim3((unsigned)nb), dim3(256), 0, s, a, r, st);
+            const int v = comb_v();
+            void (*f)(CombArgs, u64 *, u32 *) = v == 1 ? k_combine1<1> : v == 2 ? k_combine1<2> : v == 4 ? k_combine1<4>
+                                              : v == 16 ? k_combine1<16> : k_combine1<8>;
+            hipLaunchKernelGGL(f, dim3((unsigned)nb), dim3(256), 0, s, a, r, st);   // st[nb]: the ticket counter
             HIPCHK(hipGetLastError());
             return MPFFT_OK;
         }
@@ -989,6 +1025,7 @@ static int run_all(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, un
     X.single(ws);
     X.zflags = X.comb_flags(ws);
     X.zflags_n = X.comb_flag_words();
+    X.defer_double = true;   // itft + scale back to back
     int call = -1;
     {
         std::lock_guard<std::mutex> lk(g_prof_mu);
@@ -1208,6 +1245,7 @@ int mpfft_shard_stage(int stage, const mpfft_shard *sh, const uint64_t *d_i1, co
     case MPFFT_SHARD_POINTWISE: return X.pointwise();
     case MPFFT_SHARD_INV_ROWS: return X.rcount ? X.inv_rows() : MPFFT_OK;
     case MPFFT_SHARD_INV_COLUMNS:
+        X.defer_double = true;
         if ((rc = X.itft(0, P.NR, P.Tr))) return rc;
         return X.scale();
     }
