@@ -537,6 +537,24 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
 #pragma unroll
     for (int li = 0; li < LOGG; ++li) {
         const int JB = DIR == 0 ? LOGG - 1 - li : li;
+        // E == 0 for every pair of the level: the first DIF level of a pass (no pending
+        // exponents yet, rp_pend(.., 0, ..) == 0) and the first DIT level of the pass that holds
+        // the transform's last level (h == 1: rp_tw == 0).  Partners are then this thread's own
+        // registers -- no LDS round (workgroup-uniform condition).
+        if ((DIR == 0 && li == 0) || (DIR == 1 && li == 0 && a.lvl0 + LOGG == a.lbM)) {
+#pragma unroll
+            for (int pi = 0; pi < G / 2; ++pi) {
+                const int i = ((pi >> JB) << (JB + 1)) | (pi & ((1 << JB) - 1));
+                const int k = i | (1 << JB);
+#pragma unroll
+                for (int r = 0; r < PP; ++r) {
+                    const Pr y = x[k][r];
+                    pr_bfly(x[i][r], x[k][r], x[i][r], y, false);
+                }
+            }
+            if (li < 3) RP_STAMP(2 + li);
+            continue;
+        }
         // partner x_k read rotated by E: (x_i, x_k) <- (x_i + 2^E x_k, x_i - 2^E x_k)
         const int tl = rp_launder(t);
 #pragma unroll
