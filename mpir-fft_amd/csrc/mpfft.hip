@@ -69,10 +69,25 @@ struct Plan {
     bool sqrt2;         // new_mpn_mul6 plan: 4n slots, bits1 = (N - depth - 1)/2, Tr up to 2 NR
     size_t slots;       // allocated slots per operand
     size_t off_digA, off_topA, off_cbA, off_digB, off_topB, off_cbB, off_lo, off_hi, off_bg, off_bp, off_bc, bytes;
+    bool has_c;         // a third coefficient array C: the fused pointwise (k_pwss PAIR) writes there
+    size_t off_digC, off_topC, off_cbC;
     long nblk;
 };
 
 static int ilog2(long v) { int d = 0; while ((1L << d) < v) ++d; return d; }
+
+// nested negacyclic pointwise (pkernels.hpp) for big coefficients: log2 of its piece count
+static int pwss_lk_of(long l)
+{
+    const char *e = getenv("MPFFT_PWSS");
+    if (e && !strcmp(e, "0")) return 0;
+    switch (l) {
+    case 1024: return getenv("MPFFT_PWSS1024") ? 8 : 0;   // MFMA schoolbook still wins below 2048 (to measure)
+    case 2048: return 8;
+    case 4096: return 9;
+    }
+    return 0;
+}
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -165,6 +180,13 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
     p->off_digB = o; o += dig;
     p->off_topB = o; o += top;
     p->off_cbB = o; o += cbb;
+    // C: output of the fused last-row-level pointwise (single-GPU new_mpn_mul, Exec::row_fused)
+    p->has_c = !sqrt2 && p->lbC >= 2 && pwss_lk_of(p->l) != 0;
+    if (p->has_c) {
+        p->off_digC = o; o += dig;
+        p->off_topC = o; o += top;
+        p->off_cbC = o; o += cbb;
+    }
     p->off_lo = o; o += align_up((size_t)(p->total + 1) * 8, 256);
     p->off_hi = o; o += align_up((size_t)(p->total + 1) * 4, 256);
     p->nblk = (p->total + 256 * CARRY_V - 1) / (256 * CARRY_V);
@@ -248,6 +270,7 @@ struct Exec {
     hipStream_t s;
     int nw;
     View col, row;
+    View cview = {};         // the C arrays (single layout, index 0), when the plan has them
     int c0, ccount, r0, rcount, ccb, cbb;
     long cbs;
     long src_chunk = 0;      // operands are column slices (mpfft_shard.src_chunk), 0 = whole operands
@@ -255,6 +278,7 @@ struct Exec {
     long zflags_n = 0;       // (u32 words), so combine_single needs no separate fill launch
     int in_rows = 0;         // non-zero: inputs live in column rows [0, in_rows) (default: the trunc rows)
     bool defer_double = false;   // itft's top-level doubling is left to scale() (rows [dbl_lo, dbl_hi): 2^-depth)
+    bool fuse_row_last = false;  // the row DIF's last level runs inside the pointwise (k_pwss PAIR)
     long dbl_lo = 0, dbl_hi = 0;
 
     Exec(const Plan &p, hipStream_t st) : P(p), s(st) { nw = P.tpb / 64; }
@@ -290,6 +314,11 @@ struct Exec {
         col.top[1] = (int *)(ws + P.off_topB);
         col.cb[1] = (u64 *)(ws + P.off_cbB);
         row = col;
+        if (P.has_c) {
+            cview.dig[0] = (u64 *)(ws + P.off_digC);
+            cview.top[0] = (int *)(ws + P.off_topC);
+            cview.cb[0] = (u64 *)(ws + P.off_cbC);
+        }
         c0 = 0;
         ccount = (int)P.NC;
         r0 = 0;
@@ -522,17 +551,26 @@ struct Exec {
         return MPFFT_OK;
     }
 
+    // the last row level fused into k_pwss: single-GPU layout (slot pairs adjacent), a
+    // nested negacyclic pointwise, and a row pass left to apply the MFA twiddle
+    bool row_fused() const
+    {
+        static const bool off = [] { const char *e = getenv("MPFFT_FUSE_ROW"); return e && !strcmp(e, "0"); }();
+        return fuse_row_last && !off && P.has_c && cview.dig[0] && pwss_active() && ccb == P.NC;
+    }
+
     // stage 2: MFA twiddle + row DIF (length NC, root 2^(w NR)), canonical out
     int fwd_rows(int nops)
     {
         int lvl = 0;
-        while (lvl < P.lbC) {
-            int k = split(P.lbC - lvl);
+        const int L = P.lbC - (row_fused() ? 1 : 0);
+        while (lvl < L) {
+            int k = split(L - lvl);
             PassArgs a = row_args();
             a.lvl0 = lvl;
             a.tw_mode = lvl == 0 ? 1 : 0;
             // canonical pointwise inputs, except for k_pwss (it loads the reduced form)
-            if (lvl + k == P.lbC) a.canon = pwss_active() ? 0 : 1;
+            if (lvl + k == L) a.canon = pwss_active() ? 0 : 1;
             int rc = pass(a, k, 0, nops);
             if (rc) return rc;
             lvl += k;
@@ -542,17 +580,7 @@ struct Exec {
 
     // nested negacyclic pointwise (pkernels.hpp) for big coefficients: (l -> pieces 2^lk)
   public:
-    static int pwss_lk(long l)
-    {
-        const char *e = getenv("MPFFT_PWSS");
-        if (e && !strcmp(e, "0")) return 0;
-        switch (l) {
-        case 1024: return getenv("MPFFT_PWSS1024") ? 8 : 0;   // MFMA schoolbook still wins below 2048 (to measure)
-        case 2048: return 8;
-        case 4096: return 9;
-        }
-        return 0;
-    }
+    static int pwss_lk(long l) { return pwss_lk_of(l); }
 
     bool pwss_active() const
     {
@@ -566,7 +594,8 @@ struct Exec {
         if (cnt == 0) return MPFFT_OK;
         if (const int lk = pwss_lk(P.l)) {
             const int M = pw_inner_limbs(P.l, lk);
-            pw_fn f = pw_get(M, lk);
+            const bool pair = row_fused();
+            pw_fn f = pw_get(M, lk, pair ? 1 : 0);
             if (f) {
                 const size_t lds = pw_lds(M, 1 << lk, (int)P.l);
                 allow_lds((const void *)f, lds);
@@ -577,9 +606,14 @@ struct Exec {
                     HIPCHK(hipMemsetAsync(dbg, 0, (size_t)cnt * 64, s));
                 }
                 hipLaunchKernelGGL(f, dim3((unsigned)cnt), dim3(1u << lk), lds, s, row.dig[0], row.cb[0], row.top[0],
-                                   (const u64 *)row.dig[1], (const u64 *)row.cb[1], (const int *)row.top[1], (int)P.l, lk,
-                                   dbg);
+                                   (const u64 *)row.dig[1], (const u64 *)row.cb[1], (const int *)row.top[1], (int)P.l,
+                                   cview.dig[0], cview.cb[0], cview.top[0], dbg);
                 HIPCHK(hipGetLastError());
+                if (pair) {   // the product lives in C from here on (single layout: rows == columns)
+                    row.dig[0] = col.dig[0] = cview.dig[0];
+                    row.cb[0] = col.cb[0] = cview.cb[0];
+                    row.top[0] = col.top[0] = cview.top[0];
+                }
                 if (stamps) {
                     unsigned long long *h = (unsigned long long *)malloc((size_t)cnt * 64);
                     HIPCHK(hipMemcpyAsync(h, dbg, (size_t)cnt * 64, hipMemcpyDeviceToHost, s));
@@ -1026,6 +1060,7 @@ static int run_all(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, un
     X.zflags = X.comb_flags(ws);
     X.zflags_n = X.comb_flag_words();
     X.defer_double = true;   // itft + scale back to back
+    X.fuse_row_last = true;  // last row level inside the pointwise (nested negacyclic sizes)
     int call = -1;
     {
         std::lock_guard<std::mutex> lk(g_prof_mu);
@@ -1065,8 +1100,11 @@ int mpfft_stage_kernels(long n1, long n2, unsigned long depth, unsigned long w, 
     char pw[64];
     const int lk = Exec::pwss_lk(P.l);
     const char *rows = P.big && P.rpass && !(lk && pw_get(pw_inner_limbs(P.l, lk), lk)) ? "k_rpass + k_bpass (canonical last pass)" : pass;
+    const char *fz = getenv("MPFFT_FUSE_ROW");
+    const bool fused = P.lbC >= 2 && !(fz && !strcmp(fz, "0"));   // as Exec::row_fused() in run_all
     if (lk && pw_get(pw_inner_limbs(P.l, lk), lk))
-        snprintf(pw, sizeof pw, "k_pwss<%d> (nested negacyclic, K=%d)", pw_inner_limbs(P.l, lk), 1 << lk);
+        snprintf(pw, sizeof pw, "k_pwss<%d>%s (nested negacyclic, K=%d)", pw_inner_limbs(P.l, lk),
+                 fused ? " pair + last row level" : "", 1 << lk);
     else if (P.l % 256 == 0 && P.l <= 4096 && pw_kind() == 0)
         snprintf(pw, sizeof pw, "k_pwm2 (int8 MFMA)");
     else if (P.l % 128 == 0 && pw_kind() != 1)

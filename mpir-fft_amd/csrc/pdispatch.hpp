@@ -3,10 +3,12 @@
 #include <stddef.h>
 #include <stdint.h>
 
-typedef void (*pw_fn)(uint64_t *, uint64_t *, int *, const uint64_t *, const uint64_t *, const int *, int, int,
-                      unsigned long long *);
+typedef void (*pw_fn)(uint64_t *, uint64_t *, int *, const uint64_t *, const uint64_t *, const int *, int,
+                      uint64_t *, uint64_t *, int *, unsigned long long *);
 
-pw_fn pw_get(int M, int lk);       // k_pwss<M, lk> (M = inner coefficient limbs, 2^lk pieces), nullptr if not built
+// k_pwss<M, lk, fuse> (M = inner coefficient limbs, 2^lk pieces; fuse 1: the row DIF's last
+// level fused into the load, product to the C arrays), nullptr if not built
+pw_fn pw_get(int M, int lk, int fuse = 0);
 size_t pw_lds(int M, int K, int l);
 
 // Inner ring for a product mod 2^(64 l) + 1 cut into K = 2^lk pieces: the smallest M

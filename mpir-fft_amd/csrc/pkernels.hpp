@@ -330,43 +330,51 @@ __device__ __forceinline__ void pw_load_piece(u64 (&L)[M], int &T, const u64 *di
 template <int M, int LK>
 __host__ __device__ constexpr int pw_piece_limbs() { return M == 12 ? 4 : 8; }
 
-// k_pwss<M>: A[slot] <- A[slot] * B[slot] mod 2^N + 1, one workgroup of K = 2^lk threads
-// per slot; reduced-form inputs and output (HBM format of coeff.hpp).
-template <int M, int LK>
-__global__ __launch_bounds__(1 << LK) void k_pwss(u64 *digA, u64 *cbA, int *topA, const u64 *digB, const u64 *cbB,
-                                                  const int *topB, int l, int lk_unused, unsigned long long *dbg)
+// Piece t of x0 + x1 (sub = 0) or x0 - x1 (sub = 1) for two reduced-form coefficients: the
+// last DIF level of the row transform (h = 1, twiddle 1) applied piecewise -- linear, so the
+// pieces of the sum / difference are the sums / differences of the pieces (|c_t| at most
+// doubles: far inside the headroom N' >= 2B + lk + 2).  Each piece is LP limbs plus a carry
+// in {-1, 0, 1} (pw_load_piece); the LP + 1 limb result is sign-extended to M limbs, T = -1
+// for a negative value.
+template <int M, int LP>
+__device__ __forceinline__ void pw_load_pair_bfly(u64 (&L)[M], int &T, const u64 *dig, const u64 *cb, const int *top,
+                                                  long s0, int l, int cbw, int t, bool sub)
 {
-    // diagnostics (MPFFT_PW_STAMPS): thread 0 stamps the phase boundaries of this workgroup
-    unsigned long long *stamp = dbg ? dbg + 8 * (size_t)blockIdx.x : nullptr;
-#define PW_STAMP(k) do { if (stamp && threadIdx.x == 0) stamp[k] = __builtin_amdgcn_s_memtime(); } while (0)
-    PW_STAMP(0);
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    u64 A[M], B[M];
+    int Ta, Tb;
+    pw_load_piece<M, LP>(A, Ta, dig + (size_t)s0 * l, cb + (size_t)s0 * cbw, top[s0], l, t);
+    pw_load_piece<M, LP>(B, Tb, dig + (size_t)(s0 + 1) * l, cb + (size_t)(s0 + 1) * cbw, top[s0 + 1], l, t);
+    // limbs LP .. M-1 of A, B are the sign extension (carry limb LP, then 0 / ~0): add LP + 1 limbs
+    const u32 m = sub ? ~0u : 0u;
+    u32 c = sub ? 1u : 0u;
+#pragma unroll
+    for (int j = 0; j <= LP; ++j) {
+        const u32 lo = __builtin_addc((u32)A[j], (u32)B[j] ^ m, c, &c);
+        const u32 hi = __builtin_addc((u32)(A[j] >> 32), (u32)(B[j] >> 32) ^ m, c, &c);
+        L[j] = ((u64)hi << 32) | lo;
+    }
+    // the values are below 2^(64 LP + 2) in magnitude: limb LP's sign is the result's sign
+    const u64 up = (i64)L[LP] < 0 ? ~0ull : 0ull;
+#pragma unroll
+    for (int j = LP + 1; j < M; ++j) L[j] = up;
+    T = (i64)L[LP] < 0 ? -1 : 0;
+    (void)Ta;
+    (void)Tb;
+}
+
+// inner product of one slot: forward transforms of the pieces (La, Ta), (Lb, Tb), the
+// pointwise products in R', the inverse and the un-weighting; leaves the signed
+// coefficients c_t in X (limb-major, M + 1 rows) and their signs in TT (ends with a barrier)
+template <int M, int LK>
+__device__ __forceinline__ void pw_slot_product(u64 (&La)[M], int Ta, u64 (&Lb)[M], int Tb, u64 *X, u32 *Xw, int *TT,
+                                                unsigned *PP, int t, unsigned long long *stamp)
+{
+#define PW_STAMP(k) do { if (stamp && t == 0) stamp[k] = __builtin_amdgcn_s_memtime(); } while (0)
     constexpr int K = 1 << LK, lk = LK;
-    const int t = threadIdx.x;
-    const int LP = l >> lk;                      // limbs per piece
     constexpr unsigned NP = 64 * M, N2 = 2 * NP;
     const unsigned TH = NP >> lk;                // theta = 2^TH
-    u64 *X = (u64 *)smem;                        // (M + 1) K limbs (words 2M + 2 rows during the transforms)
-    u32 *Xw = (u32 *)smem;
-    int *TT = (int *)(X + (size_t)(M + 1) * K);  // K
-    unsigned *PP = (unsigned *)(TT + K);         // K
-    int *H = (int *)(PP + K);                    // l
-    const long slot = blockIdx.x;
-    const int ta = topA[slot], tb = topB[slot];
-    u64 *pa = digA + (size_t)slot * l;
-    const u64 *pb = digB + (size_t)slot * l;
-    const int lane = t & 63;
-    const int cbw = cb_words(l);
-    u64 *cbp = cbA + (size_t)slot * cbw;
-
-    // ---- pieces (reduced-form inputs) and forward transforms (A, then B in registers) ---
-    u64 La[M], Lb[M];
-    int Ta, Tb, Sa = 0, Sb = 0;   // tops, sign flags
-    constexpr int CLP = pw_piece_limbs<M, LK>();   // == LP (host: pw_inner_limbs)
-    pw_load_piece<M, CLP>(La, Ta, pa, cbp, ta, l, t);
-    pw_load_piece<M, CLP>(Lb, Tb, pb, cbB + (size_t)slot * cbw, tb, l, t);
-    __syncthreads();   // every piece read before any output limb is written (in place on A)
-    unsigned Pa = (unsigned)t * TH, Pb = Pa;   // negacyclic weight theta^t (t TH < N')
+    int Sa = 0, Sb = 0;                          // sign flags
+    unsigned Pa = (unsigned)t * TH, Pb = Pa;     // negacyclic weight theta^t (t TH < N')
     PW_STAMP(1);
     pw_transform<M, LK, 0>(La, Ta, Sa, Pa, Xw, TT, PP, TH, t);
     PW_STAMP(2);
@@ -401,10 +409,19 @@ __global__ __launch_bounds__(1 << LK) void k_pwss(u64 *digA, u64 *cbA, int *topA
     TT[t] = neg;
     __syncthreads();
     PW_STAMP(6);
+#undef PW_STAMP
+}
 
-    // ---- combine: R = sum_t c_t 2^(B t) mod 2^N + 1 -------------------------------------
-    // c_t 2^(Bt) = v_t 2^(Bt) - s_t (2^(Bt) + 2^(N' + Bt)); positions >= N wrap negated.
-    // Thread t sums output limbs m = t + K r (coalesced, consecutive per wave).
+// R = sum_t c_t 2^(B t) mod 2^N + 1 from X / TT, stored in the reduced HBM form at
+// (pa, cbp, *topp).  c_t 2^(Bt) = v_t 2^(Bt) - s_t (2^(Bt) + 2^(N' + Bt)); positions >= N
+// wrap negated.  Thread t sums output limbs m = t + K r (coalesced, consecutive per wave).
+template <int M, int LK>
+__device__ __forceinline__ void pw_slot_output(const u64 *X, const int *TT, int *H, u64 *pa, u64 *cbp, int *topp, int l,
+                                               int t)
+{
+    constexpr int K = 1 << LK;
+    const int LP = l >> LK;                      // limbs per piece
+    const int lane = t & 63;
     u64 fo[8];
     int ho[8];
     const int RPT = l / K;   // <= 8 (host)
@@ -452,10 +469,55 @@ __global__ __launch_bounds__(1 << LK) void k_pwss(u64 *digA, u64 *cbA, int *topA
             cbp[2 * (m >> 6) + 1] = nm;
         }
     }
-    if (t == 0) topA[slot] = 0;
+    if (t == 0) *topp = 0;
+}
+
+// k_pwss<M, LK, FUSE>: A[slot] <- A[slot] * B[slot] mod 2^N + 1, one workgroup of K = 2^lk
+// threads per slot; reduced-form inputs and output (HBM format of coeff.hpp).
+// FUSE 1: the inputs are the slot pairs (2i, 2i+1) of a row *before* the last level of the
+// forward row DIF (h = 1, twiddle 1); workgroup s forms the pieces of x0 + x1 (s even) or
+// x0 - x1 (s odd) of both operands on load, so that level costs no HBM pass of its own
+// (mul_fft.c:2392-2408's last FFT_radix2 level fused into the pointwise loop :3244-3253,
+// cf. the reference's row/pointwise fusion IFFT_radix2_mfa_truncate_sqrt2_combined :2745).
+// Both workgroups of a pair read all four inputs, so the product goes to C, not in place.
+// (Fusing the inverse row DIT's first level as well needs both products in one workgroup:
+// measured at 194-256 VGPRs, occupancy 2 -> 1, so the inverse side stays a pass.)
+template <int M, int LK, int FUSE>
+__global__ __launch_bounds__(1 << LK) void k_pwss(u64 *digA, u64 *cbA, int *topA, const u64 *digB, const u64 *cbB,
+                                                  const int *topB, int l, u64 *digC, u64 *cbC, int *topC,
+                                                  unsigned long long *dbg)
+{
+    // diagnostics (MPFFT_PW_STAMPS): thread 0 stamps the phase boundaries of this workgroup
+    unsigned long long *stamp = dbg ? dbg + 8 * (size_t)blockIdx.x : nullptr;
+    if (stamp && threadIdx.x == 0) stamp[0] = __builtin_amdgcn_s_memtime();
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int K = 1 << LK;
+    const int t = threadIdx.x;
+    u64 *X = (u64 *)smem;                        // (M + 1) K limbs (words 2M + 2 rows during the transforms)
+    u32 *Xw = (u32 *)smem;
+    int *TT = (int *)(X + (size_t)(M + 1) * K);  // K
+    unsigned *PP = (unsigned *)(TT + K);         // K
+    int *H = (int *)(PP + K);                    // l
+    const int cbw = cb_words(l);
+    constexpr int CLP = pw_piece_limbs<M, LK>();   // == l / K (host: pw_inner_limbs)
+    u64 La[M], Lb[M];
+    int Ta, Tb;
+    if (FUSE == 0) {
+        const long slot = blockIdx.x;
+        pw_load_piece<M, CLP>(La, Ta, digA + (size_t)slot * l, cbA + (size_t)slot * cbw, topA[slot], l, t);
+        pw_load_piece<M, CLP>(Lb, Tb, digB + (size_t)slot * l, cbB + (size_t)slot * cbw, topB[slot], l, t);
+        __syncthreads();   // every piece read before any output limb is written (in place on A)
+        pw_slot_product<M, LK>(La, Ta, Lb, Tb, X, Xw, TT, PP, t, stamp);
+        pw_slot_output<M, LK>(X, TT, H, digA + (size_t)slot * l, cbA + (size_t)slot * cbw, topA + slot, l, t);
+    } else {
+        const long slot = blockIdx.x;
+        pw_load_pair_bfly<M, CLP>(La, Ta, digA, cbA, topA, slot & ~1L, l, cbw, t, slot & 1);
+        pw_load_pair_bfly<M, CLP>(Lb, Tb, digB, cbB, topB, slot & ~1L, l, cbw, t, slot & 1);
+        pw_slot_product<M, LK>(La, Ta, Lb, Tb, X, Xw, TT, PP, t, stamp);
+        pw_slot_output<M, LK>(X, TT, H, digC + (size_t)slot * l, cbC + (size_t)slot * cbw, topC + slot, l, t);
+    }
     if (stamp) {
         __syncthreads();
-        PW_STAMP(7);
+        if (threadIdx.x == 0) stamp[7] = __builtin_amdgcn_s_memtime();
     }
-#undef PW_STAMP
 }
