@@ -52,6 +52,12 @@ CONFIGS = {
     "C4": (17, 2, 156250000),
 }
 SEED1, SEED2 = 0x1001, 0x2002
+# --mul6: the sqrt2 front end new_mpn_mul6 (mul_fft.c:3573) -- (depth, w, limbs): C3's operands
+# through a length-4n transform of the same coefficient size, and test_mul4's shape (:5559)
+CONFIGS6 = {
+    "C3": (14, 8, 20312500),
+    "M4": (14, 1, 3142656),
+}
 
 
 def stage_bytes(P, name, n1, n2):
@@ -153,18 +159,23 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default=None, choices=sorted(CONFIGS), help="default: C3 at N = 1, C4 at N > 1")
+    ap.add_argument("--config", default=None, choices=sorted(set(CONFIGS) | set(CONFIGS6)),
+                    help="default: C3 at N = 1, C4 at N > 1 (M4: --mul6 only)")
     ap.add_argument("--mode", default=None, choices=["single", "replicas", "sharded"],
                     help="N > 1: sharded (default) or independent replicas")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of oracle sampling (>= 1 call)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--e2e-reps", type=int, default=2)
+    ap.add_argument("--mul6", action="store_true",
+                    help="time new_mpn_mul6 (sqrt2 front end) on --config C3 (default) or M4 instead")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher/rendezvous check without a GPU: every rank joins a gloo group and "
                          "rank 0 prints the world it saw (tests/test_bench_launcher.py)")
     args = ap.parse_args()
 
+    if args.config and (args.config not in (CONFIGS6 if args.mul6 else CONFIGS)):
+        ap.error(f"--config {args.config} is not a {'--mul6 ' if args.mul6 else ''}configuration")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
     if args.dry_run:
@@ -197,6 +208,10 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+
+    if args.mul6:
+        print(json.dumps(bench_mul6(args, mp, dev, args.config or "C3")))
+        return
 
     if mode == "sharded":
         from importlib import import_module
@@ -319,6 +334,44 @@ def main():
     print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_mul6(args, mp, dev, cfg):
+    """One-GPU line for new_mpn_mul6 (not the headline): device-resident multiplies timed
+    like the main bench, exactness against the golden digest of the same operands."""
+    import torch
+    depth, w, nl = CONFIGS6[cfg]
+    n1 = n2 = nl
+    P = mp.plan_info6(n1, n2, depth, w)
+    a = mp.fill_random(n1, SEED1)
+    b = mp.fill_random(n2, SEED2)
+    da = torch.from_numpy(a.view(np.int64)).to(dev)
+    db = torch.from_numpy(b.view(np.int64)).to(dev)
+    dr = torch.zeros(n1 + n2, dtype=torch.int64, device=dev)
+    ws = mp.alloc_workspace6(n1, n2, depth, w, dev)
+    stream = torch.cuda.Stream(device=dev)
+    for _ in range(args.warmup):
+        mp.mul6_device(dr, da, n1, db, n2, depth, w, ws, stream=stream)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        mp.mul6_device(dr, da, n1, db, n2, depth, w, ws, stream=stream)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    got = dr.cpu().numpy().view(np.uint64)
+    want = golden_digest(cfg) if cfg in CONFIGS and CONFIGS[cfg][2] == nl else None
+    exact = hashlib.sha256(got.tobytes()).hexdigest() == want if want else None
+    balg = b_alg(P, n1, n2)
+    ms = el / args.steps * 1e3
+    return {"metric": METRIC, "value": (n1 + n2) * args.steps / el, "unit": "limbs/s", "n_gpus": 1,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic (xoshiro256** limbs, seeds 0x1001/0x2002)",
+            "config": {"workload": f"{cfg} operands via new_mpn_mul6 depth={depth} w={w} n1=n2={nl} limbs "
+                                   f"(l={P['l']}, 4n = {4 * P['n']} slots, trunc={P['trunc']})",
+                       "parallelism": "single", "entry": "new_mpn_mul6 (sqrt2, mul_fft.c:3573)"},
+            "pipeline": {"b_alg_bytes": balg, "hbm_frac_b_alg": balg / (ms * 1e-3) / HBM_PEAK},
+            "exact": exact, "exact_check": "SHA-256 vs the new_mpn_mul golden digest of the same operands"}
 
 
 if __name__ == "__main__":

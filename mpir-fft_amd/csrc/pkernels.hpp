@@ -510,7 +510,15 @@ __global__ __launch_bounds__(1 << LK) void k_pwss(u64 *digA, u64 *cbA, int *topA
         pw_slot_product<M, LK>(La, Ta, Lb, Tb, X, Xw, TT, PP, t, stamp);
         pw_slot_output<M, LK>(X, TT, H, digA + (size_t)slot * l, cbA + (size_t)slot * cbw, topA + slot, l, t);
     } else {
-        const long slot = blockIdx.x;
+        // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs (blockIdx mod 8), each
+        // with its own L2.  Blocks b and b + 8 take the two slots of one pair, so the second
+        // reads of a pair's four inputs hit the same L2 (identity on the tail of < 16 blocks).
+        const long b = blockIdx.x, nb = gridDim.x, main = nb - nb % 16;
+        long slot = b;
+        if (b < main) {
+            const long x = b & 7, j = b >> 3;
+            slot = 2 * (((j >> 1) << 3) + x) + (j & 1);
+        }
         pw_load_pair_bfly<M, CLP>(La, Ta, digA, cbA, topA, slot & ~1L, l, cbw, t, slot & 1);
         pw_load_pair_bfly<M, CLP>(Lb, Tb, digB, cbB, topB, slot & ~1L, l, cbw, t, slot & 1);
         pw_slot_product<M, LK>(La, Ta, Lb, Tb, X, Xw, TT, PP, t, stamp);
