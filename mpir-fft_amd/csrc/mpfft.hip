@@ -181,7 +181,12 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
     p->off_topB = o; o += top;
     p->off_cbB = o; o += cbb;
     // C: output of the fused last-row-level pointwise (single-GPU new_mpn_mul, Exec::row_fused)
-    p->has_c = !sqrt2 && p->lbC >= 2 && pwss_lk_of(p->l) != 0;
+    // (only where it saves a row pass: fewer passes for lbC - 1 levels than for lbC)
+    {
+        const int ml = p->maxlogg > 0 ? p->maxlogg : 1;
+        const bool saves = (p->lbC - 1 + ml - 1) / ml < (p->lbC + ml - 1) / ml;
+        p->has_c = !sqrt2 && p->lbC >= 2 && saves && pwss_lk_of(p->l) != 0;
+    }
     if (p->has_c) {
         p->off_digC = o; o += dig;
         p->off_topC = o; o += top;
@@ -1101,7 +1106,7 @@ int mpfft_stage_kernels(long n1, long n2, unsigned long depth, unsigned long w, 
     const int lk = Exec::pwss_lk(P.l);
     const char *rows = P.big && P.rpass && !(lk && pw_get(pw_inner_limbs(P.l, lk), lk)) ? "k_rpass + k_bpass (canonical last pass)" : pass;
     const char *fz = getenv("MPFFT_FUSE_ROW");
-    const bool fused = P.lbC >= 2 && !(fz && !strcmp(fz, "0"));   // as Exec::row_fused() in run_all
+    const bool fused = P.has_c && !(fz && !strcmp(fz, "0"));   // as Exec::row_fused() in run_all
     if (lk && pw_get(pw_inner_limbs(P.l, lk), lk))
         snprintf(pw, sizeof pw, "k_pwss<%d>%s (nested negacyclic, K=%d)", pw_inner_limbs(P.l, lk),
                  fused ? " pair + last row level" : "", 1 << lk);
