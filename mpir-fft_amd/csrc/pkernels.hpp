@@ -91,10 +91,21 @@ __host__ __device__ __forceinline__ void pw_combine(u64 (&L)[M], int &T, int &S,
     // Yw = -1 also reads row 2M at k = 2M - 1 (unused by the funnel): the buffer has it.
     u32 wprev = (-1 < Yw ? bw : bn)[-K] ^ (-1 < Yw ? ~smask : smask);
     u32 c = 1;
+    // every partner word is read before the first is used: all NW LDS reads in flight at once
+    // (one or two at a time, the compiler's default here, exposed the LDS latency per word)
+    u32 wv[NW];
 #pragma unroll
     for (int k = 0; k < NW; ++k) {
         const bool wr = k < Yw;
-        const u32 w = (wr ? bw : bn)[k * K] ^ (wr ? ~smask : smask);
+        wv[k] = (wr ? bw : bn)[k * K];
+#if defined(__HIP_DEVICE_COMPILE__)
+        if ((k & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+#endif
+    }
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        const bool wr = k < Yw;
+        const u32 w = wv[k] ^ (wr ? ~smask : smask);
 #if defined(__HIP_DEVICE_COMPILE__)
         const u32 o = __builtin_amdgcn_alignbit(w, wprev, sh);
 #else
