@@ -40,6 +40,19 @@ template <int M>
 __host__ __device__ __forceinline__ int pw_norm(u64 (&L)[M], int T)
 {
     const int D = T + 1;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // Fast path (the kernel is VALU-bound): a small D only moves the low word unless it
+    // under/overflows, which no lane of the wave does except with probability ~2^-30; then
+    // the top is -1 exactly.  Otherwise the full chain below.
+    {
+        const u32 w0 = (u32)L[0], n0 = w0 - (u32)D;
+        const bool spill = D > 0 ? w0 < (u32)D : (D < 0 ? n0 < (u32)(-D) : false);
+        if (!__any(spill)) {
+            L[0] = (L[0] & ~0xffffffffull) | n0;
+            return -1;
+        }
+    }
+#endif
     const u32 dh = D < 0 ? ~0u : 0u;
     u32 b = 0;
 #pragma unroll
