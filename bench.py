@@ -133,6 +133,22 @@ def pmc_traffic(cfg, kernel):
     return None, None
 
 
+def valu_util(cfg, kernel):
+    """Share of VALU issue cycles `kernel` used in the committed SQ counter pass of this config
+    (profiles/r02/pmc_<cfg>_valu/sq_valu.json: 4 cycles x SQ_INSTS_VALU / (1024 SIMDs x cycles))."""
+    p = os.path.join(ROOT, "profiles", "r02", f"pmc_{cfg.lower()}_valu", "sq_valu.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    stem = kernel.split(" ")[0].split("<")[0]
+    for name, rec in d.items():
+        if name.replace("void ", "").split("<")[0].split("(")[0] == stem and rec.get("GRBM_GUI_ACTIVE"):
+            return {"valu_util": 4 * rec["SQ_INSTS_VALU"] / (1024 * rec["GRBM_GUI_ACTIVE"] / 8),
+                    "source": os.path.relpath(p, ROOT)}
+    return None
+
+
 def golden_digest(cfg):
     p = os.path.join(ROOT, "tests", "golden", "products.json")
     try:
@@ -298,6 +314,7 @@ def main():
             "frac": dbytes / dsec / HBM_PEAK, "traffic": traffic, "traffic_source": traffic_src,
             "kernel": kern[dname], "stage": dname, "avg_ms": stage_ms[dname],
             "alg_bytes_per_launch": dbytes,
+            "compute": valu_util(cfg, kern[dname]),
             "timing": "HIP events on the library stream at the stage boundaries of the K timed multiplies"}
     balg = b_alg(P, n1, n2)
     dev_ms = float(sum(stage_ms.values()))
