@@ -11,6 +11,8 @@
  * against GMP mpn_mul, the reference's integration-test oracle (mul_fft.c:5542).
  *
  * usage: time_mul [depth w limbs iters]     -> prints "ok <ms per call>" or "MISMATCH"
+ *        time_mul --mul6 depth w limbs iters -> the same through new_mpn_mul6 (the sqrt2
+ *                                              front end, mul_fft.c:3573; test_mul4 :5559)
  *        time_mul --bad                     -> invalid parameters: new_mpn_mul must abort
  * Built by __graft_entry__.build() (gcc, -lmpfft -lgmp); run by tests/test_c_abi.py.
  */
@@ -48,6 +50,13 @@ int main(int argc, char **argv)
         printf("returned\n");               /* unreachable: new_mpn_mul aborts */
         return 0;
     }
+    int six = argc > 1 && !strcmp(argv[1], "--mul6");
+    if (six) {
+        argv++;
+        argc--;
+    }
+    void (*mul)(mp_limb_t *, mp_limb_t *, mp_size_t, mp_limb_t *, mp_size_t, mp_bitcnt_t, mp_bitcnt_t) =
+        six ? new_mpn_mul6 : new_mpn_mul;
     mp_bitcnt_t depth = argc > 4 ? strtoul(argv[1], 0, 0) : 10;
     mp_bitcnt_t w = argc > 4 ? strtoul(argv[2], 0, 0) : 3;
     mp_size_t n = argc > 4 ? strtol(argv[3], 0, 0) : 24000;
@@ -60,9 +69,9 @@ int main(int argc, char **argv)
     random_limbs(i1, n, state);
     random_limbs(i2, n, state);
 
-    new_mpn_mul(r1, i1, n, i2, n, depth, w);   /* warm-up: device context + workspace */
+    mul(r1, i1, n, i2, n, depth, w);   /* warm-up: device context + workspace */
     double t0 = now_ms();
-    for (long i = 0; i < iters; i++) new_mpn_mul(r1, i1, n, i2, n, depth, w);
+    for (long i = 0; i < iters; i++) mul(r1, i1, n, i2, n, depth, w);
     double per = (now_ms() - t0) / (iters > 0 ? iters : 1);
 
     mpn_mul(r2, i1, n, i2, n);
@@ -70,8 +79,8 @@ int main(int argc, char **argv)
         printf("MISMATCH depth=%lu w=%lu n=%ld\n", (unsigned long)depth, (unsigned long)w, (long)n);
         return 1;
     }
-    printf("ok %.3f ms per new_mpn_mul (depth=%lu w=%lu n1=n2=%ld, host pointers, H2D+D2H included)\n", per,
-           (unsigned long)depth, (unsigned long)w, (long)n);
+    printf("ok %.3f ms per %s (depth=%lu w=%lu n1=n2=%ld, host pointers, H2D+D2H included)\n", per,
+           six ? "new_mpn_mul6" : "new_mpn_mul", (unsigned long)depth, (unsigned long)w, (long)n);
     free(i1);
     gmp_randclear(state);
     return 0;
