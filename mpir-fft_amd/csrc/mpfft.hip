@@ -68,6 +68,9 @@ struct Plan {
     bool rpass;         // register-resident passes (rkernels.hpp) where they apply, l = 1024, 2048, 4096
     bool sqrt2;         // new_mpn_mul6 plan: 4n slots, bits1 = (N - depth - 1)/2, Tr up to 2 NR
     size_t slots;       // allocated slots per operand
+    // off_lo: the multi-kernel combine's limb sums, or (single-GPU default) k_combine1's
+    // look-back flags + ticket counter, cleared by the first forward column pass
+    // (Exec::zflags) -- no stage between that pass and the combine may use this region
     size_t off_digA, off_topA, off_cbA, off_digB, off_topB, off_cbB, off_lo, off_hi, off_bg, off_bp, off_bc, bytes;
     bool has_c;         // a third coefficient array C: the fused pointwise (k_pwss PAIR) writes there
     size_t off_digC, off_topC, off_cbC;
@@ -185,7 +188,7 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
     {
         const int ml = p->maxlogg > 0 ? p->maxlogg : 1;
         const bool saves = (p->lbC - 1 + ml - 1) / ml < (p->lbC + ml - 1) / ml;
-        p->has_c = !sqrt2 && p->lbC >= 2 && saves && pwss_lk_of(p->l) != 0;
+        p->has_c = p->lbC >= 2 && saves && pwss_lk_of(p->l) != 0;
     }
     if (p->has_c) {
         p->off_digC = o; o += dig;
@@ -343,6 +346,11 @@ struct Exec {
             col.top[k] += slots;
         }
         row = col;
+        if (cview.dig[0]) {
+            cview.dig[0] += slots * P.l;
+            cview.cb[0] += slots * cbw;
+            cview.top[0] += slots;
+        }
     }
 
     // rotation staging buffers for a G-coefficient pass: as many as fit in 64 KiB
@@ -1031,6 +1039,7 @@ static int run_all6(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, u
     X2.single(ws);
     X2.shift(2 * P.n);
     X2.in_rows = (int)P.NR;   // the second half's inputs are all live (FFT_radix2_truncate1_twiddle)
+    X1.fuse_row_last = X2.fuse_row_last = true;   // each half's last row level inside its pointwise
     XS.single(ws);
     XC.single(ws);
     const bool two = P2.Tr > 0;
@@ -1043,8 +1052,13 @@ static int run_all6(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, u
         if ((rc = X2.fwd_columns(nullptr, 0, nullptr, 0, 2))) return rc;
         if ((rc = X2.fwd_rows(2))) return rc;
     }
+    const bool fused = X1.row_fused();
     if ((rc = X1.pointwise())) return rc;
     if (two && (rc = X2.pointwise())) return rc;
+    if (fused) {   // the products (and everything after) live in C: X1's views now start there
+        XS.col = XS.row = X1.col;
+        XC.col = XC.row = X1.col;
+    }
     if ((rc = X1.inv_rows())) return rc;
     if (two && (rc = X2.inv_rows())) return rc;
     if ((rc = X1.itft(0, P.NR, P.NR))) return rc;
