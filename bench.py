@@ -220,10 +220,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     mode = args.mode or ("sharded" if world > 1 else "single")
     cfg = args.config or ("C4" if world > 1 else "C3")
+    # MPFFT_BENCH_SHARE_GPU=1 (rehearsal on a one-GPU box, not a measurement): every rank on
+    # cuda:0 and gloo with host-staged exchanges -- the launcher and the sharded pipeline end
+    # to end without RCCL (which does not run two ranks on one device)
+    share = os.environ.get("MPFFT_BENCH_SHARE_GPU") == "1"
+    if share:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     if args.mul6:
         print(json.dumps(bench_mul6(args, mp, dev, args.config or "C3")))

@@ -307,7 +307,7 @@ def bench(args, cfg_name, cfg, rank, world, dev):
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     # exactness: rank 0 gathers the limb ranges in rank order and hashes them (golden digest)
