@@ -113,3 +113,21 @@ def test_plan6_matches_reference_parameters(mp, oracle):
     assert checked > 50
     with pytest.raises(mp.MpfftError):
         mp.mul6(np.ones(4, np.uint64), np.ones(4, np.uint64), 6, 1)   # no GPU here: fails loudly
+
+
+def test_pwss_pair_order_is_a_permutation():
+    """k_pwss FUSE=1 (pkernels.hpp) deals slot pairs to workgroups b and b + 8 (one XCD):
+    slot(b) = 2 (8 (j >> 1) + (b & 7)) + (j & 1), j = b >> 3, identity on the last nb % 16
+    blocks.  It must be a permutation of the slots with both slots of a pair on one XCD."""
+    def slot(b, nb):
+        main = nb - nb % 16
+        if b >= main:
+            return b
+        x, j = b & 7, b >> 3
+        return 2 * (((j >> 1) << 3) + x) + (j & 1)
+    for nb in (2, 16, 18, 64, 130, 39680, 30720, 4098):
+        s = [slot(b, nb) for b in range(nb)]
+        assert sorted(s) == list(range(nb)), nb
+        where = {v: b for b, v in enumerate(s)}
+        for p in range(0, nb - nb % 16, 2):
+            assert where[p] % 8 == where[p + 1] % 8, (nb, p)
