@@ -116,37 +116,50 @@ def cpu_baseline(a, b, depth, w, budget_s):
             "cpu_model": cpu_model(), "nproc": os.cpu_count()}, ref, g
 
 
-def pmc_traffic(cfg, kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary of this config."""
+VALU_PEAK = 1024 * 32 * 2.4e9   # int32 lane-ops/s: 256 CUs x 4 SIMD-32 x 2.4 GHz (MI355X_MICROARCH.md)
+
+
+def pmc_record(cfg, kernel):
+    """The committed rocprofv3 --pmc record of `kernel` for this config (profiles/pmc_<cfg>.json,
+    built by scripts/pmc_merge.py): HBM bytes per launch and the SQ limiter counters."""
     p = os.path.join(ROOT, "profiles", f"pmc_{cfg}.json")
     if not os.path.exists(p):
         return None, None
     with open(p) as f:
         d = json.load(f)
-    want = kernel.split(" ")[0]                    # e.g. "k_pwss<20>" -> matches "void k_pwss<20, 8>(...)"
+    want = kernel.split(" ")[0]                    # e.g. "k_pwss<20>" -> matches "void k_pwss<20, 8, 1>(...)"
     stem, tmpl = want.split("<")[0], want[len(want.split("<")[0]):].strip("<>")
     for name, rec in d.get("kernels", {}).items():
         base = name.replace("void ", "").split("(")[0]
-        if base.split("<")[0] == stem and (not tmpl or base.split("<", 1)[-1].startswith(tmpl)) \
-                and "hbm_bytes_per_launch" in rec:
-            return rec["hbm_bytes_per_launch"], os.path.relpath(p, ROOT)
+        if base.split("<")[0] == stem and (not tmpl or base.split("<", 1)[-1].startswith(tmpl)):
+            return rec, os.path.relpath(p, ROOT)
     return None, None
 
 
-def valu_util(cfg, kernel):
-    """Share of VALU issue cycles `kernel` used in the committed SQ counter pass of this config
-    (profiles/r02/pmc_<cfg>_valu/sq_valu.json: 4 cycles x SQ_INSTS_VALU / (1024 SIMDs x cycles))."""
-    p = os.path.join(ROOT, "profiles", "r02", f"pmc_{cfg.lower()}_valu", "sq_valu.json")
-    if not os.path.exists(p):
-        return None
-    with open(p) as f:
-        d = json.load(f)
-    stem = kernel.split(" ")[0].split("<")[0]
-    for name, rec in d.items():
-        if name.replace("void ", "").split("<")[0].split("(")[0] == stem and rec.get("GRBM_GUI_ACTIVE"):
-            return {"valu_util": 4 * rec["SQ_INSTS_VALU"] / (1024 * rec["GRBM_GUI_ACTIVE"] / 8),
-                    "source": os.path.relpath(p, ROOT)}
-    return None
+def roofline(cfg, kernel, stage, alg_bytes, avg_ms):
+    """Roofline of the dominant kernel: HBM fraction from its algorithmic bytes per launch and
+    its live average duration; for a compute-limited kernel (VALU fraction above the HBM
+    fraction) the bound is the VALU issue rate -- SQ_INSTS_VALU per launch from the committed
+    counter pass x 64 lanes / the live duration, against 1024 SIMD-32 x 2.4 GHz."""
+    sec = avg_ms * 1e-3
+    hbm = {"achieved": alg_bytes / sec / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+           "frac": alg_bytes / sec / HBM_PEAK}
+    rec, src = pmc_record(cfg, kernel)
+    traffic = rec.get("hbm_bytes_per_launch") if rec else None
+    out = {"bound": "hbm", **hbm, "traffic": traffic, "traffic_source": src, "kernel": kernel, "stage": stage,
+           "avg_ms": avg_ms, "alg_bytes_per_launch": alg_bytes,
+           "timing": "HIP events on the library stream at the stage boundaries of K profiled multiplies "
+                     "(a separate loop after the timed one)"}
+    if rec and rec.get("SQ_INSTS_VALU"):
+        valu = rec["SQ_INSTS_VALU"] * 64 / sec
+        out["limiters"] = {k: rec[k] for k in ("valu_issue_util", "lds_util", "wait_inst_frac", "wait_any_frac",
+                                               "waves_per_simd", "clock_ghz") if k in rec}
+        out["limiters"]["source"] = src
+        if valu / VALU_PEAK > hbm["frac"]:
+            out.update({"bound": "valu", "achieved": valu / 1e12, "peak": VALU_PEAK / 1e12,
+                        "unit": "TOP/s (int32 VALU lane-ops)", "frac": valu / VALU_PEAK, "hbm": hbm,
+                        "valu_insts_per_launch": rec["SQ_INSTS_VALU"]})
+    return out
 
 
 def golden_digest(cfg):
@@ -267,12 +280,10 @@ def main():
         step()
     torch.cuda.synchronize(dev)
 
-    # timed region: K whole multiplies, one library call each; the library records a HIP
-    # event on its own stream at every stage boundary (mpfft_profile_begin), nothing else
+    # timed region: K whole multiplies, one library call each, nothing else on the stream
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    mp.profile_begin(args.steps)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -280,11 +291,21 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    stage_tot, calls = mp.profile_end()
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+
+    # stage breakdown: K more multiplies in which the library records a HIP event on its own
+    # stream at every stage boundary (mpfft_profile_begin) -- kept out of the timed loop above
+    torch.cuda.synchronize(dev)
+    mp.profile_begin(args.steps)
+    tp = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    prof_ms = (time.perf_counter() - tp) / args.steps * 1e3
+    stage_tot, calls = mp.profile_end()
     stage_ms = {k: v / max(calls, 1) for k, v in stage_tot.items()}
 
     got = dr.cpu().numpy().view(np.uint64)
@@ -316,15 +337,7 @@ def main():
     ms_step = el / args.steps * 1e3
     value = world * (n1 + n2) * args.steps / el
     dname = max(stage_ms, key=stage_ms.get)
-    dbytes = stage_bytes(P, dname, n1, n2)
-    dsec = stage_ms[dname] * 1e-3
-    traffic, traffic_src = pmc_traffic(cfg, kern[dname])
-    roof = {"bound": "hbm", "achieved": dbytes / dsec / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-            "frac": dbytes / dsec / HBM_PEAK, "traffic": traffic, "traffic_source": traffic_src,
-            "kernel": kern[dname], "stage": dname, "avg_ms": stage_ms[dname],
-            "alg_bytes_per_launch": dbytes,
-            "compute": valu_util(cfg, kern[dname]),
-            "timing": "HIP events on the library stream at the stage boundaries of the K timed multiplies"}
+    roof = roofline(cfg, kern[dname], dname, stage_bytes(P, dname, n1, n2), stage_ms[dname])
     balg = b_alg(P, n1, n2)
     dev_ms = float(sum(stage_ms.values()))
     res = {
@@ -347,6 +360,7 @@ def main():
         "pipeline": {"device_ms": dev_ms, "b_alg_bytes": balg, "hbm_frac_b_alg": balg / (dev_ms * 1e-3) / HBM_PEAK,
                      "note": "whole multiply vs the HBM roofline of the three-pass MFA (SURVEY 8d)"},
         "stages_ms": stage_ms,
+        "profiled_ms_per_step": prof_ms,
         "stage_kernels": kern,
         "e2e_host": e2e,
         "exact": exact,

@@ -29,7 +29,7 @@ typedef long mp_size_t;
 typedef unsigned long mp_bitcnt_t;
 #endif
 
-#define MPFFT_VERSION 1
+#define MPFFT_VERSION 2
 
 #define MPFFT_OK 0
 #define MPFFT_EINVAL 1          /* n1, n2 < 1; depth outside [2, 30]; n*w not a multiple of 64 */
@@ -130,7 +130,16 @@ typedef struct mpfft_shard {
     long src_chunk;           /* 0: d_i1/d_i2 are the whole operands; else this rank's column
                                  slices: for each position p < T/NC, `src_chunk` limbs from
                                  limb floor((p NC + c0) bits1 / 64) on (sharded.py) */
+    /* optional third row-layout array (NULL: none).  When set and mpfft_shard_row_fused()
+     * says so, the row DIF's last level runs inside the pointwise, whose product lands here
+     * (the caller then treats it as the row array of operand 0). */
+    uint64_t *rowc_dig, *rowc_cb;
+    int *rowc_top;
 } mpfft_shard;
+
+/* 1 if the sharded row stages fuse the last row DIF level into the pointwise for these
+ * parameters and ccb columns per row block (the caller then supplies rowc_*), else 0. */
+int mpfft_shard_row_fused(long n1, long n2, unsigned long depth, unsigned long w, int ccb);
 
 #define MPFFT_SHARD_FWD_COLUMNS 0   /* split + column DIF of both operands (column layout) */
 #define MPFFT_SHARD_FWD_ROWS 1      /* twiddle + row DIF of both operands (row layout), canonical */

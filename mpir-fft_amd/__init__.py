@@ -18,7 +18,9 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmpfft.so")
+# MPFFT_LIB=diag selects the diagnostic build libmpfft_diag.so (make DIAG=1: tuning and
+# ablation knobs for scripts/; never used by the tests, smoke() or the bench)
+LIB_PATH = os.path.join(_HERE, "libmpfft_diag.so" if os.environ.get("MPFFT_LIB") == "diag" else "libmpfft.so")
 _lib = None
 
 STAGE_FWD_COLUMNS, STAGE_FWD_ROWS, STAGE_POINTWISE, STAGE_INV_ROWS, STAGE_INV_COLUMNS, \
@@ -37,7 +39,8 @@ class _Shard(ctypes.Structure):
                 ("ccb", ctypes.c_int),
                 ("col_dig", ctypes.c_void_p * 2), ("col_cb", ctypes.c_void_p * 2), ("col_top", ctypes.c_void_p * 2),
                 ("row_dig", ctypes.c_void_p * 2), ("row_cb", ctypes.c_void_p * 2), ("row_top", ctypes.c_void_p * 2),
-                ("src_chunk", ctypes.c_long)]
+                ("src_chunk", ctypes.c_long),
+                ("rowc_dig", ctypes.c_void_p), ("rowc_cb", ctypes.c_void_p), ("rowc_top", ctypes.c_void_p)]
 
 
 class MpfftError(RuntimeError):
@@ -94,6 +97,8 @@ def lib():
         h.mpfft_fill_random.restype = None
         h.mpfft_shard_stage.argtypes = [ctypes.c_int, ctypes.POINTER(_Shard), _vp, _vp, _vp]
         h.mpfft_shard_stage.restype = ctypes.c_int
+        h.mpfft_shard_row_fused.argtypes = [_L, _L, _UL, _UL, ctypes.c_int]
+        h.mpfft_shard_row_fused.restype = ctypes.c_int
         h.mpfft_shard_combine_tmp_bytes.argtypes = [_L]
         h.mpfft_shard_combine_tmp_bytes.restype = ctypes.c_size_t
         h.mpfft_shard_combine.argtypes = [ctypes.POINTER(_Shard), ctypes.c_int, _vp, _L, _L, _L, _vp, ctypes.c_int,
@@ -352,7 +357,16 @@ def shard_desc(sh):
         d.row_cb[k] = sh["row"][k]["cb"].data_ptr()
         d.row_top[k] = sh["row"][k]["top"].data_ptr()
     d.src_chunk = int(sh.get("src_chunk", 0))
+    rc = sh.get("rowc")
+    if rc is not None:
+        d.rowc_dig, d.rowc_cb, d.rowc_top = rc["dig"].data_ptr(), rc["cb"].data_ptr(), rc["top"].data_ptr()
     return d
+
+
+def shard_row_fused(n1, n2, depth, w, ccb):
+    """True if the sharded row stages fuse the last row DIF level into the pointwise
+    (the caller then supplies a third row-layout array, `rowc`)."""
+    return bool(lib().mpfft_shard_row_fused(n1, n2, depth, w, ccb))
 
 
 def shard_stage(which, desc, d_i1, d_i2, stream=None):

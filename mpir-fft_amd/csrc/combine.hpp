@@ -4,11 +4,9 @@
 #include "coeff.hpp"
 
 // --------------------------------------------------------------------------
-// combine: r = sum_{k < len} c_k 2^(k bits1), c_k < 2^N canonical.
-// k_comb_sum: per output limb m, the 128-bit sum of the (at most a few)
-// coefficient windows covering bits [64m, 64m + 64); lo -> lo64[m], hi -> hi32[m].
-// The carry chain r = lo + (hi << 64) is then resolved by a device-wide
-// carry-lookahead (k_carry_blocks -> k_carry_scan -> k_carry_apply).
+// combine: r = sum_{k < len} c_k 2^(k bits1), c_k < 2^N canonical: per output limb the
+// 128-bit sum of the (at most a few) coefficient windows covering it, then the carry chain
+// by a decoupled look-back across blocks (k_combine1, one launch).
 // --------------------------------------------------------------------------
 struct CombArgs {
     const u64 *dig;      // canonical coefficients c_k (< 2^N) in the (blocked) row layout
@@ -22,167 +20,7 @@ struct CombArgs {
     int NC, cbb, ccb;    // row layout: k -> p = k / NC - r0, c = k % NC,
     long cbs;            //   slot = (c >> cbb) * cbs + p * ccb + (c & (ccb - 1))
     long r0;
-    u64 *lo64;           // [mcount + 1]: index i <-> limb m0 - 1 + i
-    u32 *hi32;
 };
-
-__device__ __forceinline__ const u64 *coef_ptr(const CombArgs &a, long k)
-{
-    if (k < a.kbase) return a.halo + (size_t)(k - (a.kbase - a.H)) * a.l;
-    const long p = k / a.NC - a.r0;
-    const int cc = (int)(k % a.NC);
-    const long slot = (long)(cc >> a.cbb) * a.cbs + p * a.ccb + (cc & (a.ccb - 1));
-    return a.dig + (size_t)slot * a.l;
-}
-
-// per output limb m: the 128-bit sum of the (few) coefficient windows covering
-// bits [64m, 64m + 64)  (FFT_combine_bits, mul_fft.c:207-267)
-__global__ __launch_bounds__(256) void k_comb_sum(CombArgs a)
-{
-    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > a.mcount) return;
-    const long m = a.m0 - 1 + i;
-    if (m < 0) {
-        a.lo64[i] = 0;
-        a.hi32[i] = 0;
-        return;
-    }
-    const u64 P = (u64)m * 64;
-    long klo = (P >= a.N) ? (long)((P - a.N) / a.bits1) : 0;
-    long khi = (long)((P + 63) / a.bits1);
-    if (khi > a.len - 1) khi = a.len - 1;
-    u64 slo = 0;
-    u32 shi = 0;
-    for (long k = klo; k <= khi; ++k) {
-        const u64 st = (u64)k * a.bits1;
-        const u64 *cp = coef_ptr(a, k);
-        u64 v;
-        if (st > P) {
-            v = cp[0] << (st - P);
-        } else {
-            const u64 o = P - st;
-            const long q = (long)(o >> 6);
-            const int s = (int)(o & 63);
-            const u64 w0 = (q < a.l) ? cp[q] : 0;
-            const u64 w1 = (s && q + 1 < a.l) ? cp[q + 1] : 0;
-            v = s ? (w0 >> s) | (w1 << (64 - s)) : w0;
-        }
-        u64 t;
-        shi += add_ovf(slo, v, &t);
-        slo = t;
-    }
-    a.lo64[i] = slo;
-    a.hi32[i] = shi;
-}
-
-// local limb m (0-based) of the final sum is e = lo64[m+1] + hi32[m] (arrays start one limb
-// early): value v, generate g, propagate p
-__device__ __forceinline__ void carry_limb(const u64 *lo64, const u32 *hi32, long m, u64 *v, bool *g, bool *p)
-{
-    *g = add_ovf(lo64[m + 1], (u64)hi32[m], v);
-    *p = (*v == MPF_MAXL);
-}
-
-#define CARRY_V 8  // limbs per thread in the carry kernels (256 threads -> 2048 limbs per block)
-
-// per-thread (generate, propagate) over its CARRY_V contiguous limbs
-__device__ __forceinline__ void carry_thread(const u64 *lo64, const u32 *hi32, long m0, long total, bool *G, bool *P)
-{
-    bool g = false, p = true;
-    for (int k = 0; k < CARRY_V; ++k) {
-        long m = m0 + k;
-        if (m >= total) break;
-        u64 v;
-        bool gk, pk;
-        carry_limb(lo64, hi32, m, &v, &gk, &pk);
-        g = gk || (pk && g);
-        p = p && pk;
-    }
-    *G = g;
-    *P = p;
-}
-
-__global__ __launch_bounds__(256) void k_carry_blocks(const u64 *lo64, const u32 *hi32, long total, u8 *blkG, u8 *blkP)
-{
-    __shared__ u64 scr[64];
-    const WG c = wg_ctx();
-    const long m0 = ((long)blockIdx.x * blockDim.x + c.t) * CARRY_V;
-    bool G, P;
-    carry_thread(lo64, hi32, m0, total, &G, &P);
-    u32 co;
-    wg_scan<1>(c, G, P, 0, &co, scr);
-    // block summary: generate = carry out with cin 0; propagate = every thread propagates
-    const u64 allp = __ballot(P);
-    __shared__ int pall;
-    if (c.t == 0) pall = 1;
-    __syncthreads();
-    if (c.lane == 0 && allp != ~0ull) pall = 0;
-    __syncthreads();
-    if (c.t == 0) {
-        blkG[blockIdx.x] = (u8)co;
-        blkP[blockIdx.x] = (u8)(pall && !co);
-    }
-}
-
-// single workgroup: carry into every block given the carry `cin` into the first one;
-// sum[0] = carry out of the range with cin = 0, sum[1] = every block propagates
-__global__ __launch_bounds__(1024) void k_carry_scan(const u8 *blkG, const u8 *blkP, long nblk, u8 *blkC,
-                                                     int cin, int *sum)
-{
-    __shared__ u64 scr[64];
-    const WG c = wg_ctx();
-    const long per = (nblk + c.nt - 1) / c.nt;
-    const long b0 = (long)c.t * per;
-    bool g = false, p = true;
-    for (long b = b0; b < b0 + per && b < nblk; ++b) {
-        g = blkG[b] || (blkP[b] && g);
-        p = p && blkP[b];
-    }
-    u32 co;
-    u32 ci = wg_scan<1>(c, g, p, (u32)cin, &co, scr);
-    bool run = ci & 1;
-    for (long b = b0; b < b0 + per && b < nblk; ++b) {
-        blkC[b] = (u8)run;
-        run = blkG[b] || (blkP[b] && run);
-    }
-    if (sum) {
-        u32 co0;
-        wg_scan<1>(c, g, p, 0, &co0, scr);
-        const u64 allp = __ballot(p);
-        __shared__ int pall;
-        if (c.t == 0) pall = 1;
-        __syncthreads();
-        if (c.lane == 0 && allp != ~0ull) pall = 0;
-        __syncthreads();
-        if (c.t == 0) {
-            sum[0] = (int)co0;
-            sum[1] = pall;
-        }
-    }
-}
-
-__global__ __launch_bounds__(256) void k_carry_apply(const u64 *lo64, const u32 *hi32, long total, const u8 *blkC,
-                                                     u64 *r)
-{
-    __shared__ u64 scr[64];
-    const WG c = wg_ctx();
-    const long m0 = ((long)blockIdx.x * blockDim.x + c.t) * CARRY_V;
-    bool G, P;
-    carry_thread(lo64, hi32, m0, total, &G, &P);
-    u32 co;
-    const u32 ci = wg_scan<1>(c, G, P, blkC[blockIdx.x], &co, scr);
-    bool run = ci & 1;
-    for (int k = 0; k < CARRY_V; ++k) {
-        long m = m0 + k;
-        if (m >= total) break;
-        u64 v;
-        bool gk, pk;
-        carry_limb(lo64, hi32, m, &v, &gk, &pk);
-        r[m] = v + (run ? 1 : 0);
-        run = gk || (pk && run);
-        (void)pk;
-    }
-}
 
 // --------------------------------------------------------------------------
 // k_combine1<V>: the whole single-GPU combine in one launch.  Block b owns output limbs
@@ -218,6 +56,8 @@ __device__ __forceinline__ const u64 *coef_ptr2(const CombArgs &a, long k)
     return a.dig + (size_t)slot * a.l;
 }
 
+// m: global product limb (a.m0 + local index); coefficients below kbase come from the halo
+// (a rank's combine in the sharded multiply), the rest from the row layout
 __device__ __forceinline__ void comb_limb(const CombArgs &a, long m, u64 *lo, u32 *hi)
 {
     const u64 P = (u64)m * 64;
@@ -228,7 +68,7 @@ __device__ __forceinline__ void comb_limb(const CombArgs &a, long m, u64 *lo, u3
     u32 shi = 0;
     for (long k = klo; k <= khi; ++k) {
         const u64 st = (u64)k * a.bits1;
-        const u64 *cp = coef_ptr2(a, k);
+        const u64 *cp = k < a.kbase ? a.halo + (size_t)(k - (a.kbase - a.H)) * a.l : coef_ptr2(a, k);
         u64 v;
         if (st > P) {
             v = cp[0] << (st - P);
@@ -248,8 +88,12 @@ __device__ __forceinline__ void comb_limb(const CombArgs &a, long m, u64 *lo, u3
     *hi = shi;
 }
 
+// r[i] = product limb a.m0 + i for i < a.mcount.  A rank of the sharded multiply (m0 > 0)
+// starts from carry-in 0 and the overflow of limb m0 - 1; its carry-out with that carry-in
+// ends in st[nblocks - 1] (4 + carry) and, when `allp` is given, allp[b] = 1 for every block
+// whose limbs all propagate (k_comb_summary turns both into the rank's (generate, propagate)).
 template <int CB_V>
-__global__ __launch_bounds__(256) void k_combine1(CombArgs a, u64 *r, u32 *st)
+__global__ __launch_bounds__(256) void k_combine1(CombArgs a, u64 *r, u32 *st, u32 *allp_out)
 {
     constexpr int CB_LIMBS = 256 * CB_V;
     __shared__ u64 L[CB_LIMBS];
@@ -269,14 +113,14 @@ __global__ __launch_bounds__(256) void k_combine1(CombArgs a, u64 *r, u32 *st)
         const long m = base + i;
         u64 lo = 0;
         u32 hi = 0;
-        if (m < total) comb_limb(a, m, &lo, &hi);
+        if (m < total) comb_limb(a, a.m0 + m, &lo, &hi);
         L[i] = lo;
         H[i + 1] = hi;
     }
     if (c.t == 0) {
         u64 lo = 0;
         u32 hi = 0;
-        if (base > 0) comb_limb(a, base - 1, &lo, &hi);
+        if (a.m0 + base > 0) comb_limb(a, a.m0 + base - 1, &lo, &hi);
         H[0] = hi;
     }
     __syncthreads();
@@ -297,6 +141,7 @@ __global__ __launch_bounds__(256) void k_combine1(CombArgs a, u64 *r, u32 *st)
     u32 co0;
     wg_scan<1>(c, G, Pa, 0, &co0, scr);
     const bool allp = __syncthreads_and(Pa);
+    if (allp_out && c.t == 0) allp_out[b] = allp ? 1u : 0u;
     // look-back (thread 0)
     if (c.t == 0) {
         u32 cin = 0;
@@ -332,5 +177,43 @@ __global__ __launch_bounds__(256) void k_combine1(CombArgs a, u64 *r, u32 *st)
     for (int k = 0; k < CB_V; ++k) {
         const long m = base + k * 256 + c.t;
         if (m < total) r[m] = L[k * 256 + c.t];
+    }
+}
+
+// rank summary of a k_combine1 launch over nb blocks: sum[0] = carry out with carry-in 0
+// (the last block's resolved flag), sum[1] = every limb propagates (all-ones)
+__global__ __launch_bounds__(256) void k_comb_summary(const u32 *st, const u32 *allp, long nb, int *sum)
+{
+    __shared__ int all;
+    if (threadIdx.x == 0) all = 1;
+    __syncthreads();
+    int mine = 1;
+    for (long b = threadIdx.x; b < nb; b += blockDim.x) mine &= allp[b] ? 1 : 0;
+    if (!mine) all = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        sum[0] = (int)(st[nb - 1] - 4u);
+        sum[1] = all;
+    }
+}
+
+// r[0 .. n) += 1 (the carry into a rank's limb range from the ranks below): one workgroup
+// walks 256-limb chunks until the first limb that is not all-ones (the first, almost always)
+__global__ __launch_bounds__(256) void k_carry_in(u64 *r, long n)
+{
+    __shared__ int stop;
+    for (long c0 = 0; c0 < n; c0 += 256) {
+        const long m = c0 + threadIdx.x;
+        const bool ones = m < n && r[m] == MPF_MAXL;
+        const u64 nz = __ballot(!ones && m < n);
+        if (threadIdx.x == 0) stop = 1 << 30;
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0 && nz) atomicMin(&stop, (int)(threadIdx.x + __builtin_ctzll(nz)));
+        __syncthreads();
+        const int first = stop;   // first non-all-ones limb of this chunk (or none)
+        if (m < n && (int)threadIdx.x < first) r[m] = 0;          // all-ones limbs wrap to zero
+        if (m < n && (int)threadIdx.x == first) r[m] += 1;
+        if (first < 256) return;
+        __syncthreads();
     }
 }

@@ -37,6 +37,19 @@
 // ---------------------------------------------------------------------------
 // parameters (mul_fft.c:3193-3203)
 // ---------------------------------------------------------------------------
+// Tuning / ablation / stamp knobs exist only in a diagnostic build (make DIAG=1 defines
+// MPFFT_DIAG); the shipped library never reads them, so no environment can make it skip
+// work or run an untested kernel family.
+static const char *diag_env(const char *name)
+{
+#ifdef MPFFT_DIAG
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+
 // wave kernels for coefficients of l limbs: U = ceil(l / 64) limbs per lane, full rows when l == 64 U
 static WvFns wv_fns(int U, bool full)
 {
@@ -68,28 +81,51 @@ struct Plan {
     bool rpass;         // register-resident passes (rkernels.hpp) where they apply, l = 1024, 2048, 4096
     bool sqrt2;         // new_mpn_mul6 plan: 4n slots, bits1 = (N - depth - 1)/2, Tr up to 2 NR
     size_t slots;       // allocated slots per operand
-    // off_lo: the multi-kernel combine's limb sums, or (single-GPU default) k_combine1's
+    // off_flags: k_combine1's look-back flags + ticket counter, cleared by the first forward
     // look-back flags + ticket counter, cleared by the first forward column pass
     // (Exec::zflags) -- no stage between that pass and the combine may use this region
-    size_t off_digA, off_topA, off_cbA, off_digB, off_topB, off_cbB, off_lo, off_hi, off_bg, off_bp, off_bc, bytes;
+    size_t off_digA, off_topA, off_cbA, off_digB, off_topB, off_cbB, off_flags, bytes;
     bool has_c;         // a third coefficient array C: the fused pointwise (k_pwss PAIR) writes there
     size_t off_digC, off_topC, off_cbC;
-    long nblk;
 };
 
 static int ilog2(long v) { int d = 0; while ((1L << d) < v) ++d; return d; }
 
+// pointwise kernel family.  MPFFT_POINTWISE is the one runtime selector the shipped library
+// reads (every choice is an exact product; the parity tests A/B them): auto (default),
+// pwss = the nested negacyclic k_pwss (l = 1024, 2048, 4096), mfma = int8-MFMA k_pwm2
+// (l % 256 == 0), mfma1 = k_pwm (l % 128 == 0), valu = k_pw.
+enum { PW_AUTO = 0, PW_PWSS, PW_MFMA, PW_MFMA1, PW_VALU };
+static int pw_kind()
+{
+    const char *e = getenv("MPFFT_POINTWISE");
+    if (!e) return PW_AUTO;
+    if (!strcmp(e, "pwss")) return PW_PWSS;
+    if (!strcmp(e, "mfma")) return PW_MFMA;
+    if (!strcmp(e, "mfma1")) return PW_MFMA1;
+    if (!strcmp(e, "valu")) return PW_VALU;
+    return PW_AUTO;
+}
+
 // nested negacyclic pointwise (pkernels.hpp) for big coefficients: log2 of its piece count
+// (0: another kernel).  Default from l = 2048 on; at l = 1024 the int8-MFMA schoolbook wins.
 static int pwss_lk_of(long l)
 {
-    const char *e = getenv("MPFFT_PWSS");
-    if (e && !strcmp(e, "0")) return 0;
+    const int k = pw_kind();
+    if (k != PW_AUTO && k != PW_PWSS) return 0;
     switch (l) {
-    case 1024: return getenv("MPFFT_PWSS1024") ? 8 : 0;   // MFMA schoolbook still wins below 2048 (to measure)
+    case 1024: return k == PW_PWSS ? 8 : 0;
     case 2048: return 8;
     case 4096: return 9;
     }
     return 0;
+}
+
+// the fused-pair k_pwss instance (last row DIF level on load, product to C) exists for l
+static bool pw_pair_kernel(long l)
+{
+    const int lk = pwss_lk_of(l);
+    return lk && pw_get(pw_inner_limbs(l, lk), lk, 1) != nullptr;
 }
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -135,17 +171,17 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
     p->U = Up;
     p->maxlogg = Up == 1 ? 4 : Up == 2 ? 2 : 1;   // G*U <= 8 keeps U >= 2 passes spill-free
     {
-        const char *e = getenv("MPFFT_WAVE");
+        const char *e = diag_env("MPFFT_WAVE");
         p->wave = p->l <= 256 && !(e && !strcmp(e, "0"));
     }
     if (p->wave) {
         p->wU = (int)((p->l + 63) / 64);
         p->wfull = p->l == 64L * p->wU;
         p->maxlogg = wv_fns(p->wU, p->wfull).maxlogg;
-        const char *e = getenv("MPFFT_WLOGG");
+        const char *e = diag_env("MPFFT_WLOGG");
         if (e && atoi(e) >= 1 && atoi(e) <= p->maxlogg) p->maxlogg = atoi(e);
         p->fuse_scale = p->Tr == p->NR && !sqrt2;
-        const char *el = getenv("MPFFT_LDS");
+        const char *el = diag_env("MPFFT_LDS");
         p->lds = !(el && !strcmp(el, "0"));
         if (p->lds) {
             p->maxlogg = LP_MAXLOGG;
@@ -153,7 +189,7 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
         }
     }
     {
-        const char *e = getenv("MPFFT_BIG");
+        const char *e = diag_env("MPFFT_BIG");
         const long rows = p->l / 64;
         p->big = !p->wave && p->l >= 512 && p->l % 64 == 0 && !(rows & (rows - 1)) && !(e && !strcmp(e, "0"));
     }
@@ -164,10 +200,10 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
         // columns: two 74 KB groups per CU beat one 147 KB group at l = 2048 (C3 sweep,
         // profiles/r02/sweep_blogg.txt: columns 5.97 ms vs 6.53 ms; rows 4.71 vs 4.44)
         p->maxlogg_c = lg >= 3 ? lg - 1 : lg;
-        const char *e = getenv("MPFFT_BLOGG");
+        const char *e = diag_env("MPFFT_BLOGG");
         if (e && atoi(e) >= 1 && atoi(e) <= lg) p->maxlogg = p->maxlogg_c = atoi(e);
-        const char *er = getenv("MPFFT_RPASS");
-        p->rpass = rp_maxlogg((int)p->l) > 0 && !(er && !strcmp(er, "0")) && !getenv("MPFFT_BP_STAMPS");
+        const char *er = diag_env("MPFFT_RPASS");
+        p->rpass = rp_maxlogg((int)p->l) > 0 && !(er && !strcmp(er, "0")) && !diag_env("MPFFT_BP_STAMPS");
         if (p->rpass && !e) {   // same levels per pass for columns and rows (two groups per CU either way)
             const int rl = rp_maxlogg((int)p->l) < lg ? rp_maxlogg((int)p->l) : lg;
             p->maxlogg = p->maxlogg_c = rl;
@@ -188,19 +224,14 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
     {
         const int ml = p->maxlogg > 0 ? p->maxlogg : 1;
         const bool saves = (p->lbC - 1 + ml - 1) / ml < (p->lbC + ml - 1) / ml;
-        p->has_c = p->lbC >= 2 && saves && pwss_lk_of(p->l) != 0;
+        p->has_c = p->lbC >= 2 && saves && pw_pair_kernel(p->l);
     }
     if (p->has_c) {
         p->off_digC = o; o += dig;
         p->off_topC = o; o += top;
         p->off_cbC = o; o += cbb;
     }
-    p->off_lo = o; o += align_up((size_t)(p->total + 1) * 8, 256);
-    p->off_hi = o; o += align_up((size_t)(p->total + 1) * 4, 256);
-    p->nblk = (p->total + 256 * CARRY_V - 1) / (256 * CARRY_V);
-    p->off_bg = o; o += align_up((size_t)p->nblk, 256);
-    p->off_bp = o; o += align_up((size_t)p->nblk, 256);
-    p->off_bc = o; o += align_up((size_t)p->nblk, 256);
+    p->off_flags = o; o += align_up((size_t)(p->total / 256 + 8) * 4, 256);   // k_combine1 blocks at V = 1
     p->bytes = o;
     return MPFFT_OK;
 }
@@ -242,15 +273,6 @@ static pass_fn get_pass(int U, int logg, int dir)
     case 4: return pick_pass<4>(logg, dir);
     }
     return nullptr;
-}
-
-// pointwise kernel choice: 0 = int8 MFMA register-blocked (k_pwm2, l % 256 == 0) else
-// k_pwm (l % 128 == 0), 1 = VALU MAC (k_pw), 2 = k_pwm even when k_pwm2 applies.
-// MPFFT_POINTWISE=valu / mfma1 force them (A/B parity and timing).
-static int pw_kind()
-{
-    const char *e = getenv("MPFFT_POINTWISE");
-    return (e && !strcmp(e, "valu")) ? 1 : (e && !strcmp(e, "mfma1")) ? 2 : 0;
 }
 
 // dynamic LDS above 64 KiB must be opted into per kernel (gfx950 has 160 KiB per CU)
@@ -304,13 +326,13 @@ struct Exec {
     static int comb_v()
     {
         // C3 sweep (profiles/r02/combine_cbv.txt): V = 1: 1.84 ms, 2: 0.94, 4: 0.51, 8: 0.42, 16: see there
-        static const int v = [] { const char *e = getenv("MPFFT_CB_V"); const int x = e ? atoi(e) : 8;
+        static const int v = [] { const char *e = diag_env("MPFFT_CB_V"); const int x = e ? atoi(e) : 8;
                                   return x == 1 || x == 2 || x == 4 || x == 16 ? x : 8; }();
         return v;
     }
-    long comb_blocks() const { return (P.total + 256L * comb_v() - 1) / (256L * comb_v()); }
-    u32 *comb_flags(unsigned char *ws) const { return (u32 *)(ws + P.off_lo); }
-    long comb_flag_words() const { return (comb_blocks() + 4) / 4 * 4; }
+    static long comb_blocks(long mcount) { return (mcount + 256L * comb_v() - 1) / (256L * comb_v()); }
+    u32 *comb_flags(unsigned char *ws) const { return (u32 *)(ws + P.off_flags); }
+    static long comb_flag_words(long mcount) { return (comb_blocks(mcount) + 4) / 4 * 4; }
 
     // single-GPU workspace: both layouts are the natural one
     void single(unsigned char *ws)
@@ -379,19 +401,19 @@ struct Exec {
     int pass(PassArgs a, int logg, int dir, int nops)
     {
         int rm = rpass_mode(a, logg, dir);
-        static const int rmask = [] { const char *e = getenv("MPFFT_RPASS_OFF"); return e ? atoi(e) : 0; }();
+        static const int rmask = [] { const char *e = diag_env("MPFFT_RPASS_OFF"); return e ? atoi(e) : 0; }();
         if (rm >= 0 && (rmask >> (3 * dir + rm) & 1)) rm = -1;   // diagnostics: bit 3 dir + mode off
         if (rm >= 0) {
             rp_fn f = rp_get((int)P.l, logg, dir, rm);
             if (!f) return MPFFT_EUNSUPPORTED;
-            static const size_t pad = [] { const char *e = getenv("MPFFT_RPASS_LDSPAD"); return e ? (size_t)atol(e) : 0; }();
-            static const int abl = [] { const char *e = getenv("MPFFT_ABLATE"); return e ? atoi(e) : 0; }();
+            static const size_t pad = [] { const char *e = diag_env("MPFFT_RPASS_LDSPAD"); return e ? (size_t)atol(e) : 0; }();
+            static const int abl = [] { const char *e = diag_env("MPFFT_ABLATE"); return e ? atoi(e) : 0; }();
             a.ablate = abl;
             const size_t lds = rp_lds((int)P.l, logg) + pad;   // pad: diagnostics (one workgroup per CU)
             allow_lds((const void *)f, lds);
             a.ngroups = 1 << (a.lbM - logg);
             dim3 grid((unsigned)((long)a.nsub * a.ngroups), (unsigned)nops);
-            static const bool stamps = getenv("MPFFT_RP_STAMPS") != nullptr;
+            static const bool stamps = diag_env("MPFFT_RP_STAMPS") != nullptr;
             if (stamps) return bp_stamped(f, grid, RP_NT, lds, a, logg, dir);
             hipLaunchKernelGGL(f, grid, dim3(RP_NT), lds, s, a);
             HIPCHK(hipGetLastError());
@@ -407,7 +429,7 @@ struct Exec {
             a.ngroups = 1 << (a.lbM - logg);
             dim3 grid((unsigned)((long)a.nsub * a.ngroups), (unsigned)nops);
             const unsigned nthr = (unsigned)(64 * bp_waves((int)P.l, logg));
-            static const bool stamps = getenv("MPFFT_BP_STAMPS") != nullptr;
+            static const bool stamps = diag_env("MPFFT_BP_STAMPS") != nullptr;
             if (stamps) return bp_stamped(f, grid, nthr, lds, a, logg, dir);
             hipLaunchKernelGGL(f, grid, dim3(nthr), lds, s, a);
             HIPCHK(hipGetLastError());
@@ -426,7 +448,7 @@ struct Exec {
         }
         if (P.wave) {
             {
-                const char *e = getenv("MPFFT_ABLATE");
+                const char *e = diag_env("MPFFT_ABLATE");
                 a.ablate = e ? atoi(e) : 0;
             }
             pass_fn f = wv_fns(P.wU, P.wfull).pass(logg, dir);
@@ -564,12 +586,13 @@ struct Exec {
         return MPFFT_OK;
     }
 
-    // the last row level fused into k_pwss: single-GPU layout (slot pairs adjacent), a
-    // nested negacyclic pointwise, and a row pass left to apply the MFA twiddle
+    // the last row level fused into k_pwss: slot pairs (2i, 2i + 1) of a row adjacent (any row
+    // layout with column blocks of ccb >= 2), a nested negacyclic pointwise with its fused-pair
+    // instance, and a row pass left to apply the MFA twiddle
     bool row_fused() const
     {
-        static const bool off = [] { const char *e = getenv("MPFFT_FUSE_ROW"); return e && !strcmp(e, "0"); }();
-        return fuse_row_last && !off && P.has_c && cview.dig[0] && pwss_active() && ccb == P.NC;
+        static const bool off = [] { const char *e = diag_env("MPFFT_FUSE_ROW"); return e && !strcmp(e, "0"); }();
+        return fuse_row_last && !off && P.has_c && cview.dig[0] && pw_pair_kernel(P.l) && ccb >= 2;
     }
 
     // stage 2: MFA twiddle + row DIF (length NC, root 2^(w NR)), canonical out
@@ -612,7 +635,7 @@ struct Exec {
             if (f) {
                 const size_t lds = pw_lds(M, 1 << lk, (int)P.l);
                 allow_lds((const void *)f, lds);
-                static const bool stamps = getenv("MPFFT_PW_STAMPS") != nullptr;
+                static const bool stamps = diag_env("MPFFT_PW_STAMPS") != nullptr;
                 unsigned long long *dbg = nullptr;
                 if (stamps) {   // diagnostics only: per-workgroup phase stamps, averaged on the host
                     HIPCHK(hipMalloc((void **)&dbg, (size_t)cnt * 64));
@@ -647,21 +670,21 @@ struct Exec {
                 return MPFFT_OK;
             }
         }
-        static const long pwm2_maxl = [] { const char *e = getenv("MPFFT_PWM2_MAXL"); return e ? atol(e) : 4096L; }();
-        if (P.l % 256 == 0 && P.l <= pwm2_maxl && pw_kind() == 0) {   // int8 MFMA, register-blocked: 2 fold tiles per wave
+        static const long pwm2_maxl = [] { const char *e = diag_env("MPFFT_PWM2_MAXL"); return e ? atol(e) : 4096L; }();
+        if (P.l % 256 == 0 && P.l <= pwm2_maxl && pw_kind() != PW_MFMA1 && pw_kind() != PW_VALU) {   // int8 MFMA, register-blocked: 2 fold tiles per wave
             const int nw = (int)P.l / 256;
             const int tpb = 64 * nw;
             const size_t lds = pwm_lds_bytes((int)P.l, 4, nw);
             void (*f)(u64 *, u64 *, int *, const u64 *, const int *, int, int) =
-                getenv("MPFFT_PWM2_D4") && nw <= 8 ? k_pwm2<4, 2, 4> : k_pwm2<4, 2, 2>;   // D = 4: more VGPRs, slower at C2
-            const char *ea = getenv("MPFFT_PWABLATE");   // timing experiments only: 1 = no MFMA phase
+                diag_env("MPFFT_PWM2_D4") && nw <= 8 ? k_pwm2<4, 2, 4> : k_pwm2<4, 2, 2>;   // D = 4: more VGPRs, slower at C2
+            const char *ea = diag_env("MPFFT_PWABLATE");   // timing experiments only: 1 = no MFMA phase
             allow_lds((const void *)f, lds);
             hipLaunchKernelGGL(f, dim3((unsigned)cnt), dim3(tpb), lds, s, row.dig[0], row.cb[0], row.top[0],
                                (const u64 *)row.dig[1], (const int *)row.top[1], (int)P.l, ea ? atoi(ea) : 0);
             HIPCHK(hipGetLastError());
             return MPFFT_OK;
         }
-        if (P.l % 128 == 0 && pw_kind() != 1) {   // int8 MFMA Toeplitz product
+        if (P.l % 128 == 0 && pw_kind() != PW_VALU) {   // int8 MFMA Toeplitz product
             const int nw = std::min((int)P.l / 128, 16);
             const int tpb = 64 * nw;
             const int U = (int)P.l / tpb;
@@ -885,107 +908,87 @@ struct Exec {
         return MPFFT_OK;
     }
 
-    // combine the canonical coefficients of the row layout (A) into limbs [m0, m0+mcount)
-    // with carry-in `cin`; tmp arrays: lo (mcount+1 u64), hi (mcount+1 u32), 3 block-flag
-    // arrays of nblk bytes, sum[2] int.
-    int combine(u64 *r, long m0, long mcount, long kbase, const u64 *halo, int H, u64 *lo, u32 *hi, u8 *bg,
-                u8 *bp, u8 *bc, int cin, int *sum, bool apply)
+    // combine the canonical coefficients of the row layout (A) into product limbs
+    // [m0, m0 + mcount) of r (r[0] = limb m0) in one k_combine1 launch: window sums plus a
+    // decoupled look-back carry chain, carry-in 0.  `kbase` is the first coefficient of the
+    // row layout, `halo` the H coefficients before it (a rank of the sharded multiply).
+    // st: the look-back flags (comb_flag_words(mcount) u32, zeroed here unless `cleared`);
+    // allp (or null): per-block all-ones flags for the rank summary.
+    int combine1(u64 *r, long m0, long mcount, long kbase, const u64 *halo, int H, u32 *st, bool cleared, u32 *allp)
     {
-        const long nblk = (mcount + 256 * CARRY_V - 1) / (256 * CARRY_V);
-        if (!apply) {
-            CombArgs a;
-            a.dig = row.dig[0];
-            a.l = (int)P.l;
-            a.N = P.N;
-            a.bits1 = P.bits1;
-            a.len = P.len;
-            a.m0 = m0;
-            a.mcount = mcount;
-            a.kbase = kbase;
-            a.halo = halo;
-            a.H = H;
-            a.NC = (int)P.NC;
-            a.cbb = cbb;
-            a.ccb = ccb;
-            a.cbs = cbs;
-            a.r0 = r0;
-            a.lo64 = lo;
-            a.hi32 = hi;
-            hipLaunchKernelGGL(k_comb_sum, dim3((unsigned)((mcount + 1 + 255) / 256)), dim3(256), 0, s, a);
-            HIPCHK(hipGetLastError());
-            hipLaunchKernelGGL(k_carry_blocks, dim3((unsigned)nblk), dim3(256), 0, s, (const u64 *)lo,
-                               (const u32 *)hi, mcount, bg, bp);
-            HIPCHK(hipGetLastError());
-            if (sum) {   // rank summary only (carry-in decided by the caller)
-                hipLaunchKernelGGL(k_carry_scan, dim3(1), dim3(1024), 0, s, (const u8 *)bg, (const u8 *)bp, nblk,
-                                   bc, 0, sum);
-                HIPCHK(hipGetLastError());
-                return MPFFT_OK;
-            }
-        }
-        hipLaunchKernelGGL(k_carry_scan, dim3(1), dim3(1024), 0, s, (const u8 *)bg, (const u8 *)bp, nblk, bc, cin,
-                           (int *)nullptr);
-        HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_carry_apply, dim3((unsigned)nblk), dim3(256), 0, s, (const u64 *)lo, (const u32 *)hi,
-                           mcount, (const u8 *)bc, r);
+        CombArgs a;
+        a.dig = row.dig[0];
+        a.l = (int)P.l;
+        a.N = P.N;
+        a.bits1 = P.bits1;
+        a.len = P.len;
+        a.m0 = m0;
+        a.mcount = mcount;
+        a.kbase = kbase;
+        a.halo = halo;
+        a.H = H;
+        a.NC = (int)P.NC;
+        a.cbb = cbb;
+        a.ccb = ccb;
+        a.cbs = cbs;
+        a.r0 = r0;
+        const long nb = comb_blocks(mcount);
+        if (!cleared) HIPCHK(hipMemsetAsync(st, 0, (size_t)comb_flag_words(mcount) * 4, s));   // one fill
+        const int v = comb_v();
+        void (*f)(CombArgs, u64 *, u32 *, u32 *) = v == 1 ? k_combine1<1> : v == 2 ? k_combine1<2>
+                                                 : v == 4 ? k_combine1<4> : v == 16 ? k_combine1<16> : k_combine1<8>;
+        hipLaunchKernelGGL(f, dim3((unsigned)nb), dim3(256), 0, s, a, r, st, allp);   // st[nb]: the ticket counter
         HIPCHK(hipGetLastError());
         return MPFFT_OK;
     }
 
     int combine_single(u64 *r, unsigned char *ws)
     {
-        static const bool multi = [] { const char *e = getenv("MPFFT_COMBINE"); return e && !strcmp(e, "multi"); }();
-        if (!multi) {   // one launch: window sums + decoupled look-back carries (k_combine1)
-            CombArgs a;
-            a.dig = row.dig[0];
-            a.l = (int)P.l;
-            a.N = P.N;
-            a.bits1 = P.bits1;
-            a.len = P.len;
-            a.m0 = 0;
-            a.mcount = P.total;
-            a.kbase = 0;
-            a.halo = nullptr;
-            a.H = 0;
-            a.NC = (int)P.NC;
-            a.cbb = cbb;
-            a.ccb = ccb;
-            a.cbs = cbs;
-            a.r0 = r0;
-            a.lo64 = nullptr;
-            a.hi32 = nullptr;
-            const long nb = comb_blocks();
-            u32 *st = comb_flags(ws);   // (nb + 1) flags, inside the lo64 scratch of the multi-kernel path
-            if (zflags != st)           // not already cleared by the first forward column pass
-                HIPCHK(hipMemsetAsync(st, 0, (size_t)comb_flag_words() * 4, s));   // whole 16-byte words: one fill
-            const int v = comb_v();
-            void (*f)(CombArgs, u64 *, u32 *) = v == 1 ? k_combine1<1> : v == 2 ? k_combine1<2> : v == 4 ? k_combine1<4>
-                                              : v == 16 ? k_combine1<16> : k_combine1<8>;
-            hipLaunchKernelGGL(f, dim3((unsigned)nb), dim3(256), 0, s, a, r, st);   // st[nb]: the ticket counter
-            HIPCHK(hipGetLastError());
-            return MPFFT_OK;
-        }
-        return combine(r, 0, P.total, 0, nullptr, 0, (u64 *)(ws + P.off_lo), (u32 *)(ws + P.off_hi),
-                       ws + P.off_bg, ws + P.off_bp, ws + P.off_bc, 0, nullptr, false);
+        u32 *st = comb_flags(ws);
+        return combine1(r, 0, P.total, 0, nullptr, 0, st, zflags == st, nullptr);
     }
 };
 
-// Stage profiling (mpfft_profile_begin/end): while active, run_all records a HIP event
-// on its own stream at every stage boundary of every multiply -- the timed calls are
-// otherwise unchanged -- and profile_end sums the per-stage times.
+// Stage profiling (mpfft_profile_begin/end): while active, each multiply claims a call slot
+// and records a HIP event on its own stream at every stage boundary -- the timed calls are
+// otherwise unchanged -- and profile_end sums the per-stage times of the calls that
+// recorded every boundary.  A claimed slot keeps its own event pointer (taken under the
+// lock), and profile_begin refuses to reallocate while claimed calls are still running.
 struct StageProf {
     bool on = false;
-    int cap = 0, used = 0;
+    int cap = 0, used = 0, inflight = 0;
     hipEvent_t *ev = nullptr;   // cap * (MPFFT_NSTAGES + 1)
+    int *marks = nullptr;       // per claimed call: boundaries recorded (MPFFT_NSTAGES + 1 = complete)
 };
 static std::mutex g_prof_mu;
 static StageProf g_prof;
 
-static void prof_mark(int call, int stage, hipStream_t s)
-{
-    if (call < 0) return;
-    (void)hipEventRecord(g_prof.ev[call * (MPFFT_NSTAGES + 1) + stage], s);
-}
+struct ProfCall {
+    int call = -1;
+    hipEvent_t *ev = nullptr;
+    int marks = 0;
+    ProfCall()
+    {
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        if (g_prof.on && g_prof.used < g_prof.cap) {
+            call = g_prof.used++;
+            ev = g_prof.ev + (size_t)call * (MPFFT_NSTAGES + 1);
+            ++g_prof.inflight;
+        }
+    }
+    void mark(int stage, hipStream_t s)
+    {
+        if (call < 0) return;
+        if (hipEventRecord(ev[stage], s) == hipSuccess && stage == marks) ++marks;
+    }
+    ~ProfCall()
+    {
+        if (call < 0) return;
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        g_prof.marks[call] = marks;
+        --g_prof.inflight;
+    }
+};
 
 // the sqrt2 top level (kernels.hpp k_s2op): one workgroup per k in [k0, k0 + cnt)
 static int s2_launch(const Plan &P, const Exec &X, int op, const u64 *srcA, const u64 *srcB, long k0, long cnt,
@@ -1077,30 +1080,26 @@ static int run_all(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, un
     Exec X(P, s);
     X.single(ws);
     X.zflags = X.comb_flags(ws);
-    X.zflags_n = X.comb_flag_words();
+    X.zflags_n = X.comb_flag_words(P.total);
     X.defer_double = true;   // itft + scale back to back
     X.fuse_row_last = true;  // last row level inside the pointwise (nested negacyclic sizes)
-    int call = -1;
-    {
-        std::lock_guard<std::mutex> lk(g_prof_mu);
-        if (g_prof.on && g_prof.used < g_prof.cap) call = g_prof.used++;
-    }
+    ProfCall pc;
     int rc;
-    prof_mark(call, 0, s);
+    pc.mark(0, s);
     if ((rc = X.fwd_columns(d_i1, P.n1, d_i2, P.n2, 2))) return rc;
-    prof_mark(call, 1, s);
+    pc.mark(1, s);
     if ((rc = X.fwd_rows(2))) return rc;
-    prof_mark(call, 2, s);
+    pc.mark(2, s);
     if ((rc = X.pointwise())) return rc;
-    prof_mark(call, 3, s);
+    pc.mark(3, s);
     if ((rc = X.inv_rows())) return rc;
-    prof_mark(call, 4, s);
+    pc.mark(4, s);
     if ((rc = X.itft(0, P.NR, P.Tr))) return rc;
-    prof_mark(call, 5, s);
+    pc.mark(5, s);
     if ((rc = X.scale())) return rc;
-    prof_mark(call, 6, s);
+    pc.mark(6, s);
     rc = X.combine_single(d_r, ws);
-    prof_mark(call, 7, s);
+    pc.mark(7, s);
     return rc;
 }
 
@@ -1119,14 +1118,14 @@ int mpfft_stage_kernels(long n1, long n2, unsigned long depth, unsigned long w, 
     char pw[64];
     const int lk = Exec::pwss_lk(P.l);
     const char *rows = P.big && P.rpass && !(lk && pw_get(pw_inner_limbs(P.l, lk), lk)) ? "k_rpass + k_bpass (canonical last pass)" : pass;
-    const char *fz = getenv("MPFFT_FUSE_ROW");
+    const char *fz = diag_env("MPFFT_FUSE_ROW");
     const bool fused = P.has_c && !(fz && !strcmp(fz, "0"));   // as Exec::row_fused() in run_all
     if (lk && pw_get(pw_inner_limbs(P.l, lk), lk))
         snprintf(pw, sizeof pw, "k_pwss<%d>%s (nested negacyclic, K=%d)", pw_inner_limbs(P.l, lk),
                  fused ? " pair + last row level" : "", 1 << lk);
-    else if (P.l % 256 == 0 && P.l <= 4096 && pw_kind() == 0)
+    else if (P.l % 256 == 0 && P.l <= 4096 && pw_kind() != PW_MFMA1 && pw_kind() != PW_VALU)
         snprintf(pw, sizeof pw, "k_pwm2 (int8 MFMA)");
-    else if (P.l % 128 == 0 && pw_kind() != 1)
+    else if (P.l % 128 == 0 && pw_kind() != PW_VALU)
         snprintf(pw, sizeof pw, "k_pwm (int8 MFMA)");
     else if (P.l % 2 == 0 && P.l >= 32)
         snprintf(pw, sizeof pw, "k_pw (VALU)");
@@ -1134,46 +1133,55 @@ int mpfft_stage_kernels(long n1, long n2, unsigned long depth, unsigned long w, 
         snprintf(pw, sizeof pw, "k_pointwise (VALU)");
     const char *pair = P.rpass ? "k_rpair" : P.wave ? "k_wpair" : "k_pairop";
     const char *scale = P.fuse_scale ? "(fused into the last inverse column pass)" : P.rpass ? "k_rscale" : P.wave ? "k_wscale" : "k_scale";
-    static const bool multi = [] { const char *e = getenv("MPFFT_COMBINE"); return e && !strcmp(e, "multi"); }();
-    snprintf(buf, len, "%s;%s;%s;%s;%s + %s;%s;%s", pass, rows, pw, pass, pass, pair, scale,
-             multi ? "k_comb_sum + k_carry_*" : "k_combine1");
+    snprintf(buf, len, "%s;%s;%s;%s;%s + %s;%s;%s", pass, rows, pw, pass, pass, pair, scale, "k_combine1");
     return MPFFT_OK;
 }
 
 int mpfft_profile_begin(int max_calls)
 {
     std::lock_guard<std::mutex> lk(g_prof_mu);
-    if (max_calls < 1) return MPFFT_EINVAL;
-    const int need = max_calls * (MPFFT_NSTAGES + 1);
+    if (max_calls < 1 || g_prof.inflight > 0) return MPFFT_EINVAL;
+    const int per = MPFFT_NSTAGES + 1;
     if (g_prof.cap < max_calls) {
-        for (int i = 0; i < g_prof.cap * (MPFFT_NSTAGES + 1); ++i) (void)hipEventDestroy(g_prof.ev[i]);
+        for (int i = 0; i < g_prof.cap * per; ++i) (void)hipEventDestroy(g_prof.ev[i]);
         free(g_prof.ev);
-        g_prof.ev = (hipEvent_t *)calloc((size_t)need, sizeof(hipEvent_t));
+        free(g_prof.marks);
         g_prof.cap = 0;
-        for (int i = 0; i < need; ++i)
-            if (hipEventCreate(&g_prof.ev[i]) != hipSuccess) return MPFFT_EHIP;
+        g_prof.ev = (hipEvent_t *)calloc((size_t)max_calls * per, sizeof(hipEvent_t));
+        g_prof.marks = (int *)calloc((size_t)max_calls, sizeof(int));
+        if (!g_prof.ev || !g_prof.marks) return MPFFT_ENOMEM;
+        for (int i = 0; i < max_calls * per; ++i)
+            if (hipEventCreate(&g_prof.ev[i]) != hipSuccess) {   // no leak: destroy what was made
+                for (int j = 0; j < i; ++j) (void)hipEventDestroy(g_prof.ev[j]);
+                return MPFFT_EHIP;
+            }
         g_prof.cap = max_calls;
     }
+    for (int c = 0; c < g_prof.cap; ++c) g_prof.marks[c] = 0;
     g_prof.used = 0;
     g_prof.on = true;
     return MPFFT_OK;
 }
 
+// sums the calls that recorded every stage boundary (a call that failed part-way is skipped)
 int mpfft_profile_end(float *stage_ms, int *calls)
 {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_prof.on = false;
     for (int k = 0; k < MPFFT_NSTAGES; ++k) stage_ms[k] = 0.f;
+    int done = 0;
     for (int c = 0; c < g_prof.used; ++c) {
-        hipEvent_t *e = g_prof.ev + c * (MPFFT_NSTAGES + 1);
+        if (g_prof.marks[c] != MPFFT_NSTAGES + 1) continue;
+        hipEvent_t *e = g_prof.ev + (size_t)c * (MPFFT_NSTAGES + 1);
         if (hipEventSynchronize(e[MPFFT_NSTAGES]) != hipSuccess) return MPFFT_EHIP;
         for (int k = 0; k < MPFFT_NSTAGES; ++k) {
             float ms = 0.f;
             if (hipEventElapsedTime(&ms, e[k], e[k + 1]) != hipSuccess) return MPFFT_EHIP;
             stage_ms[k] += ms;
         }
+        ++done;
     }
-    if (calls) *calls = g_prof.used;
+    if (calls) *calls = done;
     return MPFFT_OK;
 }
 
@@ -1285,7 +1293,20 @@ static int shard_exec(Exec &X, const mpfft_shard *sh)
     X.cbb = ilog2(sh->ccb);
     X.cbs = (long)sh->rcount * sh->ccb;
     X.src_chunk = sh->src_chunk;
+    if (sh->rowc_dig && sh->rowc_cb && sh->rowc_top) {   // fused last row level (mpfft_shard_row_fused)
+        X.cview.dig[0] = sh->rowc_dig;
+        X.cview.cb[0] = sh->rowc_cb;
+        X.cview.top[0] = sh->rowc_top;
+        X.fuse_row_last = true;
+    }
     return MPFFT_OK;
+}
+
+int mpfft_shard_row_fused(long n1, long n2, unsigned long depth, unsigned long w, int ccb)
+{
+    Plan P;
+    if (make_plan(&P, n1, n2, depth, w)) return 0;
+    return P.has_c && pw_pair_kernel(P.l) && ccb >= 2 && !(P.NC % ccb);
 }
 
 int mpfft_shard_stage(int stage, const mpfft_shard *sh, const uint64_t *d_i1, const uint64_t *d_i2, void *stream)
@@ -1311,9 +1332,8 @@ int mpfft_shard_stage(int stage, const mpfft_shard *sh, const uint64_t *d_i1, co
 
 size_t mpfft_shard_combine_tmp_bytes(long mcount)
 {
-    const long nblk = (mcount + 256 * CARRY_V - 1) / (256 * CARRY_V);
-    return align_up((size_t)(mcount + 1) * 8, 256) + align_up((size_t)(mcount + 1) * 4, 256) +
-           3 * align_up((size_t)nblk, 256);
+    if (mcount < 1) return 0;
+    return align_up((size_t)Exec::comb_flag_words(mcount) * 4, 256) + align_up((size_t)Exec::comb_blocks(mcount) * 4, 256);
 }
 
 int mpfft_shard_combine(const mpfft_shard *sh, int phase, uint64_t *d_r, long m0, long mcount, long kbase,
@@ -1325,17 +1345,25 @@ int mpfft_shard_combine(const mpfft_shard *sh, int phase, uint64_t *d_r, long m0
     if (rc) return rc;
     if (mcount < 1 || m0 < 0 || m0 + mcount > P.total) return MPFFT_EINVAL;
     if (tmp_bytes < mpfft_shard_combine_tmp_bytes(mcount)) return MPFFT_ENOMEM;
+    if (phase == 0 && (!d_sum || (kbase > 0 && (!halo || H < 1)))) return MPFFT_EINVAL;
     (void)hipGetLastError();
     Exec X(P, (hipStream_t)stream);
     if ((rc = shard_exec(X, sh))) return rc;
-    unsigned char *t = (unsigned char *)d_tmp;
-    const long nblk = (mcount + 256 * CARRY_V - 1) / (256 * CARRY_V);
-    u64 *lo = (u64 *)t;
-    u32 *hi = (u32 *)(t + align_up((size_t)(mcount + 1) * 8, 256));
-    u8 *bg = (u8 *)hi + align_up((size_t)(mcount + 1) * 4, 256);
-    u8 *bp = bg + align_up((size_t)nblk, 256);
-    u8 *bc = bp + align_up((size_t)nblk, 256);
-    return X.combine(d_r, m0, mcount, kbase, halo, H, lo, hi, bg, bp, bc, cin, d_sum, phase == 1);
+    u32 *st = (u32 *)d_tmp;
+    u32 *allp = (u32 *)((unsigned char *)d_tmp + align_up((size_t)Exec::comb_flag_words(mcount) * 4, 256));
+    hipStream_t s = (hipStream_t)stream;
+    if (phase == 0) {   // the rank's limbs with carry-in 0, and its (generate, propagate) summary
+        if ((rc = X.combine1(d_r, m0, mcount, kbase, halo, H, st, false, allp))) return rc;
+        hipLaunchKernelGGL(k_comb_summary, dim3(1), dim3(256), 0, s, (const u32 *)st, (const u32 *)allp,
+                           Exec::comb_blocks(mcount), d_sum);
+        HIPCHK(hipGetLastError());
+        return MPFFT_OK;
+    }
+    if (cin) {          // the carry from the ranks below: +1 over the run of all-ones limbs
+        hipLaunchKernelGGL(k_carry_in, dim3(1), dim3(256), 0, s, d_r, mcount);
+        HIPCHK(hipGetLastError());
+    }
+    return MPFFT_OK;
 }
 
 // host-pointer entry with status.  One context per device (SURVEY 8b "Threading"):

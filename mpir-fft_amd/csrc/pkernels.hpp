@@ -275,6 +275,17 @@ __device__ __forceinline__ unsigned pw_mod(unsigned a, unsigned n)
     return a >= n ? a - n : a;
 }
 
+// Exchange ordering inside one wave: a wave's LDS instructions execute in issue order, so a
+// level whose butterfly partners share a wave (h < 64) needs no workgroup barrier -- only a
+// compiler fence that keeps this level's reads after its publish and before the next
+// publish.  Levels with h >= 64 exchange across waves and keep both __syncthreads.
+__device__ __forceinline__ void pw_wave_sync()
+{
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
 template <int M, int LK, int DIR>
 __device__ __forceinline__ void pw_transform(u64 (&L)[M], int &T, int &S, unsigned &P, u32 *Xw, int *TT, unsigned *PP,
                                              unsigned TH, int t)
@@ -290,9 +301,10 @@ __device__ __forceinline__ void pw_transform(u64 (&L)[M], int &T, int &S, unsign
         const int qt = t & ~h;                       // top index of the pair
         // (qt mod h) 2^j < K/2, times 2 TH: below N' (= K TH): no reduction needed
         const unsigned tw = (unsigned)((qt & (h - 1)) << j) * (2 * TH);
+        const bool cross = h >= 64;                  // partner in another wave
         pw_publish<M, LK>(L, T, S, Xw, TT, t);
         PP[t] = P;
-        __syncthreads();
+        if (cross) __syncthreads(); else pw_wave_sync();
         const unsigned Pq = PP[q];
         unsigned E;
         if (DIR == 0) {
@@ -307,7 +319,7 @@ __device__ __forceinline__ void pw_transform(u64 (&L)[M], int &T, int &S, unsign
             pw_combine<M, LK>(L, T, S, top ? 1 : -1, Xw, TT, q, E);
             if (!top) P = pw_mod(P + N2 - tw, N2);
         }
-        __syncthreads();
+        if (cross) __syncthreads(); else pw_wave_sync();
     }
 }
 
@@ -420,9 +432,9 @@ __device__ __forceinline__ void pw_slot_product(u64 (&La)[M], int Ta, u64 (&Lb)[
         const unsigned un = (unsigned)t * TH + lk;   // < N' + lk
         const unsigned F = pw_mod(Pz + N2 - un, N2);
         pw_publish<M, LK>(Z, Tz, Sz, Xw, TT, t);
-        __syncthreads();
+        pw_wave_sync();                                  // own column only
         pw_combine<M, LK>(Z, Tz, Sz, 0, Xw, TT, t, F);   // clears the sign flag
-        __syncthreads();
+        __syncthreads();                                 // the u64 rows below cross columns
     }
     // signed coefficient c_t = v - s p', v in [0, 2^N'], s = (v > 2^(N'-1))
     const int zt = pw_canon<M>(Z, Tz);

@@ -98,12 +98,16 @@ class ShardedMul:
         p = plan
         self.col = [backend.alloc_coeffs(p.col_slots()) for _ in range(2)]
         self.row = [backend.alloc_coeffs(p.row_slots(rank)) for _ in range(2)]
+        # the row DIF's last level fused into the pointwise, as on one GPU: the product lands in
+        # a third row array, which then serves as operand 0's row array (swapped after the stage)
+        self.fused = bool(getattr(backend, "row_fused", lambda: False)())
+        self.rowc = backend.alloc_coeffs(p.row_slots(rank)) if self.fused else None
 
     def shard_desc(self):
         p, d = self.p, self.rank
         return dict(n1=p.n1, n2=p.n2, depth=p.depth, w=p.w, c0=d * p.C, ccount=p.C,
                     r0=p.rows[d], rcount=p.rcount(d), ccb=p.C, col=self.col, row=self.row,
-                    src_chunk=p.chunk if self.sliced else 0)
+                    src_chunk=p.chunk if self.sliced else 0, rowc=self.rowc)
 
     # all-to-all #1 / #3: column layout rows [r_d, r_{d+1}) -> rank d's row layout block;
     # every field (and operand) of one exchange goes in one batch of point-to-point ops
@@ -132,20 +136,33 @@ class ShardedMul:
                 plan.append((send, recv))
         self.comm.exchange(plan)
 
-    def run(self, i1, i2):
+    def run(self, i1, i2, mark=None):
         """i1, i2: this rank's operand column slices (ShardPlan.slice_operand; the full
-        operands when sliced=False), backend arrays.  Returns (m0, limbs)."""
+        operands when sliced=False), backend arrays.  Returns (m0, limbs).
+        mark(name), when given, is called after each phase (bench.py's per-phase events)."""
         p, be, sh = self.p, self.be, self.shard_desc()
+        mark = mark or (lambda name: None)
         be.stage("fwd_columns", sh, i1, i2)
+        mark("fwd_columns")
         self._col_to_row((0, 1), ("dig", "cb", "top"))
+        mark("exchange1")
         be.stage("fwd_rows", sh, i1, i2)
+        mark("fwd_rows")
         be.stage("pointwise", sh, i1, i2)
+        mark("pointwise")
+        if self.fused:   # the product is in rowc: it becomes operand 0's row array
+            self.row[0], self.rowc = self.rowc, self.row[0]
+            sh["rowc"] = self.rowc
         be.stage("inv_rows", sh, i1, i2)
+        mark("inv_rows")
         self._row_to_col((0,), ("dig", "cb", "top"))
+        mark("exchange2")
         be.stage("inv_columns", sh, i1, i2)
+        mark("inv_columns")
         self._col_to_row((0,), ("dig",))                   # canonical coefficients: limbs only
         # halo: the last H coefficients of every rank's range, all-gathered
         halo_all = self.comm.all_gather(be.tail_coeffs(sh, p.H))
+        mark("exchange3")
         d = self.rank
         m0, mcount = p.M[d], p.M[d + 1] - p.M[d]
         kbase = p.rows[d] * p.NC
@@ -157,6 +174,7 @@ class ShardedMul:
             g, pr = int(sums[e][0]), int(sums[e][1])
             cin = 1 if (g or (pr and cin)) else 0
         limbs = be.combine(sh, 1, m0, mcount, kbase, halo, p.H if d else 0, cin=cin)
+        mark("combine")
         return m0, limbs
 
 
@@ -228,6 +246,10 @@ class GpuBackend:
     def width(self, field, p):
         return {"dig": p.l, "cb": p.cbw, "top": 1}[field]
 
+    def row_fused(self):
+        p = self.p
+        return self.mp.shard_row_fused(p.n1, p.n2, p.depth, p.w, p.C)
+
     def alloc_coeffs(self, slots):
         t = self.torch
         p = self.p
@@ -271,6 +293,15 @@ class GpuBackend:
         return self._r
 
 
+# algorithmic HBM bytes of one rank's phase (1/world of the whole multiply's)
+def _phase_bytes(P, name, n1, n2, world):
+    T, l = P["trunc"], P["l"]
+    blk = 8 * l + 4
+    whole = {"fwd_columns": 8 * (n1 + n2) + 2 * T * blk, "fwd_rows": 4 * T * blk, "pointwise": 3 * T * blk,
+             "inv_rows": 2 * T * blk, "inv_columns": 4 * T * blk, "combine": T * blk + 8 * (n1 + n2)}
+    return whole[name] / world if name in whole else None
+
+
 def bench(args, cfg_name, cfg, rank, world, dev):
     """`bench.py --gpus N` (N > 1) / `--mode sharded`: one multiply of `cfg` split over
     all ranks (strong scaling).  Returns rank 0's JSON record (driver contract fields)."""
@@ -288,36 +319,77 @@ def bench(args, cfg_name, cfg, rank, world, dev):
     a = mp.fill_random(nl, 0x1001)
     b = mp.fill_random(nl, 0x2002)
     # only this rank's column slices of the operands travel to its GPU (1/world of each)
-    da = torch.from_numpy(plan.slice_operand(a, rank).view(np.int64)).to(dev)
-    db = torch.from_numpy(plan.slice_operand(b, rank).view(np.int64)).to(dev)
+    ha = plan.slice_operand(a, rank)
+    hb = plan.slice_operand(b, rank)
     del a, b
+    da = torch.from_numpy(ha.view(np.int64)).to(dev)
+    db = torch.from_numpy(hb.view(np.int64)).to(dev)
     be = GpuBackend(mp, plan, dev)
-    comm = TorchComm(host_staging=(world > 1 and dist.get_backend() != "nccl")) if world > 1 else _SoloComm()
+    rccl = world > 1 and dist.get_backend() == "nccl"
+    comm = TorchComm(host_staging=(world > 1 and not rccl)) if world > 1 else _SoloComm()
     job = ShardedMul(plan, rank, be, comm)
+
+    def sync_all():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev if rccl else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
     for _ in range(args.warmup):
         job.run(da, db)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    sync_all()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         m0, limbs = job.run(da, db)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    sync_all()
+    el = max_over_ranks(time.perf_counter() - t0)
+
+    # per-phase device time of one more multiply: torch events on the current stream (the
+    # library's kernels and the exchanges run there), max over ranks per phase
+    evs = [("start", torch.cuda.Event(enable_timing=True))]
+    evs[0][1].record()
+
+    def mark(name):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        evs.append((name, e))
+    job.run(da, db, mark=mark)
+    sync_all()
+    phase_ms = {evs[i][0]: max_over_ranks(evs[i - 1][1].elapsed_time(evs[i][1])) for i in range(1, len(evs))}
+    P = mp.plan_info(nl, nl, depth, w)
+    comp = {k: v for k, v in phase_ms.items() if not k.startswith("exchange")}
+    dname = max(comp, key=comp.get)
+    dbytes = _phase_bytes(P, dname, nl, nl, world)
+    roof = {"bound": "hbm", "achieved": dbytes / (comp[dname] * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
+            "frac": dbytes / (comp[dname] * 1e-3) / 8.0e12, "traffic": None, "stage": dname,
+            "avg_ms": comp[dname], "alg_bytes_per_launch": dbytes,
+            "note": "the slowest rank's dominant phase (all of its launches) vs one GPU's HBM peak; "
+                    "algorithmic bytes = the phase's whole-multiply bytes / world"}
+
+    # end to end from host operands: this rank's column slices H2D, the multiply, its limbs D2H
+    sync_all()
+    t1 = time.perf_counter()
+    ea = torch.from_numpy(ha.view(np.int64)).to(dev)
+    eb = torch.from_numpy(hb.view(np.int64)).to(dev)
+    _, el2 = job.run(ea, eb)
+    host_limbs = el2.cpu()
+    sync_all()
+    e2e_ms = max_over_ranks(time.perf_counter() - t1) * 1e3
+    del ea, eb, host_limbs
+
     # exactness: rank 0 gathers the limb ranges in rank order and hashes them (golden digest)
     exact = None
     if not getattr(args, "no_check", False):
-        gpu_comm = world > 1 and dist.get_backend() == "nccl"
         if rank == 0:
             parts = [limbs.cpu().numpy().view(np.uint64)]
             for d in range(1, world):
-                buf = torch.empty(plan.M[d + 1] - plan.M[d], dtype=torch.int64, device=dev if gpu_comm else "cpu")
+                buf = torch.empty(plan.M[d + 1] - plan.M[d], dtype=torch.int64, device=dev if rccl else "cpu")
                 dist.recv(buf, src=d)
                 parts.append(buf.cpu().numpy().view(np.uint64))
             h = hashlib.sha256()
@@ -331,10 +403,15 @@ def bench(args, cfg_name, cfg, rank, world, dev):
             except OSError:
                 exact = None
         elif world > 1:
-            dist.send(limbs if gpu_comm else limbs.cpu(), dst=0)
-    P = mp.plan_info(nl, nl, depth, w)
+            dist.send(limbs if rccl else limbs.cpu(), dst=0)
     A = P["trunc"] * (P["l"] + 1) * 8
     balg = 8 * A + 32 * nl
+    if world == 1:
+        comm_label = "local exchanges (world 1)"
+    elif rccl:
+        comm_label = "RCCL over xGMI"
+    else:
+        comm_label = "gloo, host-staged (ranks sharing one GPU: a rehearsal, not a measurement)"
     return {"metric": "limbs/s for new_mpn_mul N×N-bit at 1/2/4/8 MI355X; % HBM roofline",
             "value": 2 * nl * args.steps / el, "unit": "limbs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
@@ -342,11 +419,17 @@ def bench(args, cfg_name, cfg, rank, world, dev):
             "data": "synthetic (xoshiro256** limbs, seeds 0x1001/0x2002)",
             "config": {"workload": f"{cfg_name}: sharded new_mpn_mul depth={depth} w={w} n1=n2={nl} limbs "
                                    f"(l={P['l']}, NC x NR = {P['NC']} x {P['NR']}, trunc={P['trunc']})",
-                       "parallelism": f"MFA columns x{world}, operand column slices, 3 batched point-to-point exchanges + halo all-gather "
-                                      f"({'RCCL' if world > 1 and dist.get_backend() == 'nccl' else 'local'})"},
+                       "parallelism": f"MFA columns x{world}, operand column slices, 3 batched point-to-point "
+                                      f"exchanges + halo all-gather ({comm_label})",
+                       "row_fused": job.fused},
+            "roofline": roof,
+            "phases_ms": phase_ms,
             "pipeline": {"b_alg_bytes": balg,
                          "hbm_frac_b_alg": balg / (el / args.steps) / (world * 8.0e12),
                          "note": "whole multiply vs the aggregate HBM roofline of the ranks (SURVEY 8d)"},
+            "e2e_host": {"ms": e2e_ms, "limbs_per_s": 2 * nl / (e2e_ms * 1e-3),
+                         "note": "per rank: its operand column slices H2D, the multiply, its product limbs D2H "
+                                 "(host slicing excluded); max over ranks"},
             "exact": exact}
 
 

@@ -1,12 +1,13 @@
 """Diagnostics (GPU box): forward-stage values of one shape with some k_rpass modes
 switched off (MPFFT_RPASS_OFF), compared slot by slot mod p with an exact reference
-(gpu_stages spec).  usage: python tests/dbg_rpass.py depth w n1 n2 [stage]"""
+(gpu_stages spec).  Needs the diagnostic build (make -C mpir-fft_amd/csrc DIAG=1) and
+MPFFT_LIB=diag.  usage: MPFFT_LIB=diag python scripts/dbg_rpass.py depth w n1 n2 [stage]"""
 import os
 import sys
 
 import numpy as np
 
-HERE = os.path.dirname(os.path.abspath(__file__))
+HERE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests")
 sys.path.insert(0, os.path.dirname(HERE))
 sys.path.insert(0, HERE)
 from helpers import chunks, log2, revbin, to_int  # noqa: E402

@@ -2,7 +2,8 @@
 """Per-kernel average of rocprofv3 --pmc counters (counter_collection.csv).
 usage: pmc_summary.py <dir-with-csv> [out.json]
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch; on gfx950 FETCH_SIZE reports half the
-bytes of a wide coalesced read (MI355X_MICROARCH.md "HBM"), so hbm_read_bytes = 2 * 1024 * FETCH_SIZE."""
+bytes of a wide coalesced read (MI355X_MICROARCH.md "HBM"), so hbm_read_bytes = 2 * 1024 * FETCH_SIZE.
+duration_ns: the dispatch's own start/end stamps in the same (profiled) pass."""
 import collections
 import csv
 import glob
@@ -18,7 +19,10 @@ for fn in files:
         for r in csv.DictReader(f):
             k = r["Kernel_Name"]
             acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
-            disp[k].add((fn, r["Dispatch_Id"]))
+            key = (fn, r["Dispatch_Id"])
+            if key not in disp[k] and r.get("End_Timestamp"):
+                acc[k]["duration_ns"] += float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+            disp[k].add(key)
 out = {}
 for k, cs in acc.items():
     n = len(disp[k])

@@ -114,13 +114,19 @@ def _pattern(kind, l, N, rng):
     return v, 0
 
 
-@pytest.mark.parametrize("kind", ["mfma", "mfma1", "valu"])
-@pytest.mark.parametrize("depth,w", [(11, 1), (9, 16), (8, 64), (7, 256), (6, 1024), (5, 4096), (6, 4096)])
+PW_CASES = [(k, d, w) for k in ("mfma", "mfma1", "valu")
+            for d, w in ((11, 1), (9, 16), (8, 64), (7, 256), (6, 1024), (5, 4096), (6, 4096))] + \
+           [("pwss", 6, 1024), ("pwss", 5, 4096), ("pwss", 6, 4096), ("auto", 5, 4096), ("auto", 6, 4096)]
+
+
+@pytest.mark.parametrize("kind,depth,w", PW_CASES)
 def test_pointwise_direct(mp, torch_dev, kind, depth, w):
     """The pointwise stage alone on hand-placed canonical inputs (every pair of the
-    special values 0, 1, 2^N - 1, 2^N, 0x80.. and 0x7f.. bytes, random), for the
-    int8-MFMA kernels (k_pwm2 when l % 256 == 0, k_pwm when l % 128 == 0 or
-    MPFFT_POINTWISE=mfma1) and the VALU kernel (MPFFT_POINTWISE=valu)."""
+    special values 0, 1, 2^N - 1, 2^N, 0x80.. and 0x7f.. bytes, random), for every
+    kernel family MPFFT_POINTWISE selects: the int8-MFMA kernels (mfma: k_pwm2 when
+    l % 256 == 0; mfma1: k_pwm), the VALU schoolbook (valu: k_pw) and the nested
+    negacyclic k_pwss (pwss: l = 1024, 2048, 4096 -- the default from l = 2048 on,
+    "auto").  The kernel that ran is checked through mpfft_stage_kernels."""
     import torch
     from gpu_stages import _cbs, _val_reduced
     mx = max_limbs(depth, w)
@@ -148,8 +154,16 @@ def test_pointwise_direct(mp, torch_dev, kind, depth, w):
     db = torch.zeros(n2, dtype=torch.int64, device=torch_dev)
     dr = torch.zeros(n1 + n2, dtype=torch.int64, device=torch_dev)
     old = os.environ.get("MPFFT_POINTWISE")
-    os.environ["MPFFT_POINTWISE"] = kind
+    if kind == "auto":
+        os.environ.pop("MPFFT_POINTWISE", None)
+    else:
+        os.environ["MPFFT_POINTWISE"] = kind
     try:
+        ran = mp.stage_kernels(n1, n2, depth, w)["pointwise"].split(" ")[0].split("<")[0]
+        mfma1 = "k_pwm" if l % 128 == 0 else "k_pw"
+        expect = {"pwss": "k_pwss", "auto": "k_pwss", "valu": "k_pw", "mfma1": mfma1,
+                  "mfma": "k_pwm2" if l % 256 == 0 else mfma1}[kind]
+        assert ran == expect, (kind, l, ran)
         mp.stage(mp.STAGE_POINTWISE, da, db, dr, n1, n2, depth, w, ws)
         torch.cuda.synchronize()
     finally:

@@ -9,7 +9,6 @@ import socket
 import numpy as np
 import pytest
 
-from helpers import max_limbs
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -21,8 +20,11 @@ def _exact(a, b, limbs):
 
 
 @pytest.mark.parametrize("depth,w,n1,n2", [(6, 2, 7, 6), (8, 1, 100, 90), (11, 8, 261952, 261952),
-                                          (11, 1, 16384, 16384), (10, 3, 1000, 17)])
-def test_sharded_world1(mp, depth, w, n1, n2):
+                                          (11, 1, 16384, 16384), (10, 3, 1000, 17),
+                                          (15, 4, 2000000, 1900000), (13, 32, 1000000, 1000000)])
+def test_sharded_world1(mp, oracle, depth, w, n1, n2):
+    """World 1 through the sharded code path (column slices, local exchanges) at l = 32 ... 4096:
+    (15, 4) is a C2/C3-shaped l = 2048 case, (13, 32) an l = 4096 case with 8 row levels."""
     import torch
     from mpir_fft_amd.sharded import ShardPlan, ShardedMul, GpuBackend, _SoloComm
     dev = torch.device("cuda:0")
@@ -33,7 +35,37 @@ def test_sharded_world1(mp, depth, w, n1, n2):
     sa, sb = plan.slice_operand(a, 0), plan.slice_operand(b, 0)
     m0, limbs = job.run(torch.from_numpy(sa.view(np.int64)).to(dev), torch.from_numpy(sb.view(np.int64)).to(dev))
     torch.cuda.synchronize()
-    assert m0 == 0 and _exact(a, b, limbs.cpu().numpy())
+    got = limbs.cpu().numpy().view(np.uint64)
+    assert m0 == 0 and (got == oracle.gmp_mul(a, b)).all()
+
+
+def test_sharded_world1_c4_digest(mp):
+    """BASELINE configs[4] (10^10-bit, depth 17, w 2, l = 4096) through the column-sharded
+    code path at world 1 -- operand column slices, the fused-split loaders at l = 4096, the
+    local exchanges and the rank combine -- against the committed GMP digest of C4."""
+    import hashlib
+    import json
+    import torch
+    from mpir_fft_amd.sharded import ShardPlan, ShardedMul, GpuBackend, _SoloComm
+    with open(os.path.join(HERE, "golden", "products.json")) as f:
+        want = {c["name"]: c for c in json.load(f)}["C4"]
+    depth, w, nl = want["depth"], want["w"], want["n1"]
+    dev = torch.device("cuda:0")
+    plan = ShardPlan(mp, nl, nl, depth, w, 1)
+    a = mp.fill_random(nl, int(want["seed1"], 16))
+    sa = torch.from_numpy(plan.slice_operand(a, 0).view(np.int64)).to(dev)
+    del a
+    b = mp.fill_random(nl, int(want["seed2"], 16))
+    sb = torch.from_numpy(plan.slice_operand(b, 0).view(np.int64)).to(dev)
+    del b
+    job = ShardedMul(plan, 0, GpuBackend(mp, plan, dev), _SoloComm())
+    m0, limbs = job.run(sa, sb)
+    torch.cuda.synchronize()
+    got = limbs.cpu().numpy().view(np.uint64)
+    assert m0 == 0 and len(got) == 2 * nl
+    assert hashlib.sha256(got.tobytes()).hexdigest() == want["sha256"]
+    del job, sa, sb, limbs
+    torch.cuda.empty_cache()
 
 
 def _free_port():
@@ -48,6 +80,7 @@ def _worker(rank, world, port, depth, w, n1, n2, q):
     import sys
     sys.path.insert(0, os.path.dirname(HERE))
     sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch
@@ -71,8 +104,9 @@ def _worker(rank, world, port, depth, w, n1, n2, q):
         bufs = [torch.zeros(max(sizes), dtype=torch.int64) for _ in range(world)]
         dist.all_gather(bufs, pad)
         if rank == 0:
-            prod = np.concatenate([bufs[d][: sizes[d]].numpy() for d in range(world)])
-            q.put("ok" if _exact(a, b, prod) else "mismatch")
+            import oracle as O
+            prod = np.concatenate([bufs[d][: sizes[d]].numpy() for d in range(world)]).view(np.uint64)
+            q.put("ok" if (prod == O.gmp_mul(a, b)).all() else "mismatch")
     except Exception as e:  # pragma: no cover
         q.put("error " + repr(e))
         raise
@@ -80,7 +114,11 @@ def _worker(rank, world, port, depth, w, n1, n2, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,depth,w,n1,n2", [(2, 11, 8, 261952, 261952), (2, 9, 2, 2000, 1500)])
+# two ranks on one GPU, exchanges host-staged through gloo: C1's shape (l = 256), a small
+# unbalanced case, a depth-15 w-4 case (l = 2048, the C2/C3 coefficient size) and a depth-13
+# w-32 case (l = 4096, the C4 coefficient size, 8 row levels)
+@pytest.mark.parametrize("world,depth,w,n1,n2", [(2, 11, 8, 261952, 261952), (2, 9, 2, 2000, 1500),
+                                                 (2, 15, 4, 2000000, 2000000), (2, 13, 32, 1000000, 1000000)])
 def test_sharded_two_ranks_one_gpu(world, depth, w, n1, n2):
     import torch.multiprocessing as tmp
     ctx = tmp.get_context("spawn")
