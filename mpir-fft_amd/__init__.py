@@ -20,7 +20,9 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # MPFFT_LIB=diag selects the diagnostic build libmpfft_diag.so (make DIAG=1: tuning and
 # ablation knobs for scripts/; never used by the tests, smoke() or the bench)
-LIB_PATH = os.path.join(_HERE, "libmpfft_diag.so" if os.environ.get("MPFFT_LIB") == "diag" else "libmpfft.so")
+_LIBSEL = os.environ.get("MPFFT_LIB", "")
+LIB_PATH = os.path.join(_HERE, "libmpfft_diag.so" if _LIBSEL == "diag" else
+                        _LIBSEL if _LIBSEL.endswith(".so") else "libmpfft.so")   # a path: A/B scripts
 _lib = None
 
 STAGE_FWD_COLUMNS, STAGE_FWD_ROWS, STAGE_POINTWISE, STAGE_INV_ROWS, STAGE_INV_COLUMNS, \

@@ -559,7 +559,21 @@ struct Exec {
     }
 
     // stage 1: split + forward truncated column DIF (length NR, root 2^(w NC))
-    int fwd_columns(const u64 *srcA, long nA, const u64 *srcB, long nB, int nops)
+    // operand `op` alone (0 or 1) in slot 0 of the pass arguments, one grid row (nops = 1);
+    // op < 0: both operands (grid rows 0, 1)
+    static PassArgs only(PassArgs a, int op)
+    {
+        if (op == 1) {
+            a.dig[0] = a.dig[1];
+            a.cb[0] = a.cb[1];
+            a.top[0] = a.top[1];
+            a.src[0] = a.src[1];
+            a.nsrc[0] = a.nsrc[1];
+        }
+        return a;
+    }
+
+    int fwd_columns(const u64 *srcA, long nA, const u64 *srcB, long nB, int nops, int op = -1)
     {
         int lvl = 0;
         while (lvl < P.lbR) {
@@ -579,7 +593,8 @@ struct Exec {
             a.lvl0 = lvl;
             a.rho = (u64)P.w * P.NC;
             a.need = (int)P.Tr;
-            int rc = pass(a, k, 0, nops);
+            if (op == 1) a.zp = nullptr;   // the combine flags are cleared by operand 0's pass
+            int rc = op < 0 ? pass(a, k, 0, nops) : pass(only(a, op), k, 0, 1);
             if (rc) return rc;
             lvl += k;
         }
@@ -596,7 +611,7 @@ struct Exec {
     }
 
     // stage 2: MFA twiddle + row DIF (length NC, root 2^(w NR)), canonical out
-    int fwd_rows(int nops)
+    int fwd_rows(int nops, int op = -1)
     {
         int lvl = 0;
         const int L = P.lbC - (row_fused() ? 1 : 0);
@@ -607,7 +622,7 @@ struct Exec {
             a.tw_mode = lvl == 0 ? 1 : 0;
             // canonical pointwise inputs, except for k_pwss (it loads the reduced form)
             if (lvl + k == L) a.canon = pwss_active() ? 0 : 1;
-            int rc = pass(a, k, 0, nops);
+            int rc = op < 0 ? pass(a, k, 0, nops) : pass(only(a, op), k, 0, 1);
             if (rc) return rc;
             lvl += k;
         }
@@ -1074,7 +1089,16 @@ static int run_all6(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, u
     return XC.combine_single(d_r, ws);
 }
 
-static int run_all(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, unsigned char *ws, hipStream_t s)
+// Host operands (mul_host): operand 2's copy from the host runs on the context's copy stream
+// while operand 1's forward columns and rows run on `s`; operand 2's passes wait for it.
+struct HostB {
+    const u64 *h;       // host limbs of operand 2 (null: d_i2 is already on the device)
+    hipStream_t cs;     // copy stream
+    hipEvent_t ready;   // recorded on cs after the copy
+};
+
+static int run_all(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, unsigned char *ws, hipStream_t s,
+                   const HostB *hb = nullptr)
 {
     if (P.sqrt2) return run_all6(P, d_r, d_i1, d_i2, ws, s);
     Exec X(P, s);
@@ -1086,9 +1110,20 @@ static int run_all(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, un
     ProfCall pc;
     int rc;
     pc.mark(0, s);
-    if ((rc = X.fwd_columns(d_i1, P.n1, d_i2, P.n2, 2))) return rc;
-    pc.mark(1, s);
-    if ((rc = X.fwd_rows(2))) return rc;
+    if (hb && hb->h) {   // operand 1's forward transform overlaps operand 2's H2D copy
+        HIPCHK(hipMemcpyAsync((void *)d_i2, hb->h, (size_t)P.n2 * 8, hipMemcpyHostToDevice, hb->cs));
+        HIPCHK(hipEventRecord(hb->ready, hb->cs));
+        if ((rc = X.fwd_columns(d_i1, P.n1, d_i2, P.n2, 1, 0))) return rc;
+        if ((rc = X.fwd_rows(1, 0))) return rc;
+        HIPCHK(hipStreamWaitEvent(s, hb->ready, 0));
+        if ((rc = X.fwd_columns(d_i1, P.n1, d_i2, P.n2, 1, 1))) return rc;
+        if ((rc = X.fwd_rows(1, 1))) return rc;
+        pc.mark(1, s);
+    } else {
+        if ((rc = X.fwd_columns(d_i1, P.n1, d_i2, P.n2, 2))) return rc;
+        pc.mark(1, s);
+        if ((rc = X.fwd_rows(2))) return rc;
+    }
     pc.mark(2, s);
     if ((rc = X.pointwise())) return rc;
     pc.mark(3, s);
@@ -1376,6 +1411,8 @@ struct DevCtx {
     u64 *io = nullptr;
     size_t io_bytes = 0;
     hipStream_t stream = nullptr;
+    hipStream_t copy = nullptr;   // operand 2's H2D beside operand 1's forward transform
+    hipEvent_t ready = nullptr;
 };
 static const int MPFFT_MAX_DEV = 64;
 static DevCtx g_dev[MPFFT_MAX_DEV];
@@ -1402,13 +1439,19 @@ static int mul_host(const Plan &P, uint64_t *r1, const uint64_t *i1, long n1, co
     DevCtx &C = g_dev[dev];
     std::lock_guard<std::mutex> lk(C.mu);
     if (!C.stream) HIPCHK(hipStreamCreateWithFlags(&C.stream, hipStreamNonBlocking));
+    if (!C.copy) HIPCHK(hipStreamCreateWithFlags(&C.copy, hipStreamNonBlocking));
+    if (!C.ready) HIPCHK(hipEventCreateWithFlags(&C.ready, hipEventDisableTiming));
     if ((rc = ensure_buf((void **)&C.ws, &C.ws_bytes, P.bytes))) return rc;
     if ((rc = ensure_buf((void **)&C.io, &C.io_bytes, (size_t)2 * (n1 + n2) * 8))) return rc;
     u64 *d_i1 = C.io, *d_i2 = C.io + n1, *d_r = C.io + n1 + n2;
     HIPCHK(hipMemcpyAsync(d_i1, i1, (size_t)n1 * 8, hipMemcpyHostToDevice, C.stream));
-    HIPCHK(hipMemcpyAsync(d_i2, i2, (size_t)n2 * 8, hipMemcpyHostToDevice, C.stream));
-    rc = run_all(P, d_r, d_i1, d_i2, C.ws, C.stream);
-    if (rc) return rc;
+    HostB hb{P.sqrt2 ? nullptr : i2, C.copy, C.ready};
+    if (P.sqrt2) HIPCHK(hipMemcpyAsync(d_i2, i2, (size_t)n2 * 8, hipMemcpyHostToDevice, C.stream));
+    rc = run_all(P, d_r, d_i1, d_i2, C.ws, C.stream, &hb);
+    if (rc) {
+        (void)hipStreamSynchronize(C.copy);   // the copy stream never outlives the call
+        return rc;
+    }
     HIPCHK(hipMemcpyAsync(r1, d_r, (size_t)(n1 + n2) * 8, hipMemcpyDeviceToHost, C.stream));
     HIPCHK(hipStreamSynchronize(C.stream));
     return MPFFT_OK;

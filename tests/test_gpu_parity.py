@@ -168,7 +168,7 @@ def test_pointwise_direct(mp, torch_dev, kind, depth, w):
         torch.cuda.synchronize()
     finally:
         if old is None:
-            del os.environ["MPFFT_POINTWISE"]
+            os.environ.pop("MPFFT_POINTWISE", None)
         else:
             os.environ["MPFFT_POINTWISE"] = old
     dig = digA.cpu().numpy().view(np.uint64)
