@@ -152,8 +152,8 @@ def roofline(cfg, kernel, stage, alg_bytes, avg_ms):
                      "(a separate loop after the timed one)"}
     if rec and rec.get("SQ_INSTS_VALU"):
         valu = rec["SQ_INSTS_VALU"] * 64 / sec
-        out["limiters"] = {k: rec[k] for k in ("valu_issue_util", "lds_util", "wait_inst_frac", "wait_any_frac",
-                                               "waves_per_simd", "clock_ghz") if k in rec}
+        out["limiters"] = {k: rec[k] for k in ("valu_issue_util", "valu_cycle_util_est", "lds_util", "wait_inst_frac",
+                                               "wait_any_frac", "waves_per_simd", "clock_ghz") if k in rec}
         out["limiters"]["source"] = src
         if valu / VALU_PEAK > hbm["frac"]:
             out.update({"bound": "valu", "achieved": valu / 1e12, "peak": VALU_PEAK / 1e12,

@@ -1111,10 +1111,11 @@ static int run_all(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, un
     int rc;
     pc.mark(0, s);
     if (hb && hb->h) {   // operand 1's forward transform overlaps operand 2's H2D copy
-        HIPCHK(hipMemcpyAsync((void *)d_i2, hb->h, (size_t)P.n2 * 8, hipMemcpyHostToDevice, hb->cs));
-        HIPCHK(hipEventRecord(hb->ready, hb->cs));
+        // kernels first: a copy from pageable memory may hold the calling thread until it is done
         if ((rc = X.fwd_columns(d_i1, P.n1, d_i2, P.n2, 1, 0))) return rc;
         if ((rc = X.fwd_rows(1, 0))) return rc;
+        HIPCHK(hipMemcpyAsync((void *)d_i2, hb->h, (size_t)P.n2 * 8, hipMemcpyHostToDevice, hb->cs));
+        HIPCHK(hipEventRecord(hb->ready, hb->cs));
         HIPCHK(hipStreamWaitEvent(s, hb->ready, 0));
         if ((rc = X.fwd_columns(d_i1, P.n1, d_i2, P.n2, 1, 1))) return rc;
         if ((rc = X.fwd_rows(1, 1))) return rc;

@@ -689,13 +689,127 @@ __global__ __launch_bounds__(RP_NT) void k_rpair(PairArgs a)
     }, (short *)smem, t);
 }
 
+// ---- canonicalisation of a slot-form coefficient by all the waves of a workgroup -----------
+// Wave-level: f[64 u0 ...] += sv (sub: -= sv), the carry rippling upward until it dies
+// (almost always in the first limb); returns 1 if it ran off limb l - 1 (the value left
+// [0, 2^N) upward, resp. downward).  Same ballot look-ahead as bp_canon.
+__device__ int rp_ripple(const BSlot &b, int l, int u0, bool sub, u64 sv, int lane)
+{
+    const int rows = l >> 6;
+    u64 run = 0;
+    for (int u = u0; u < rows; ++u) {
+        const int m = 64 * u + lane;
+        const bool first = u == u0 && lane == 0;
+        const u64 f = b.f[m];
+        bool g, p;
+        if (first) {
+            u64 t2;
+            g = sub ? f < sv : add_ovf(f, sv, &t2);
+            p = sub ? f == sv : (f + sv) == MPF_MAXL;
+        } else {
+            g = false;
+            p = sub ? f == 0 : f == MPF_MAXL;
+        }
+        const u64 X = __ballot(g), Yp = X | __ballot(p);
+        u64 s1, s2;
+        const bool o1 = add_ovf(X, Yp, &s1);
+        const bool o2 = add_ovf(s1, run, &s2);
+        const u64 add = (first ? sv : 0) + (((s2 ^ X ^ Yp) >> lane) & 1);
+        b.f[m] = sub ? f - add : f + add;
+        run = (o1 | o2) ? 1 : 0;
+        if (!run) return 0;   // wave-uniform
+    }
+    return 1;
+}
+
+// bp_canon (mpn_normmod_2expp1, mul_fft.c:272) spread over NWV waves: wave w sweeps rows
+// [w R, (w + 1) R) of the slot form (limb f_m + carry c_m into it) with no inc/dec chain
+// entering its first row, the carry of the limb below computed directly.  A chain that
+// leaves a segment (its run-out; probability ~2^-64 per boundary) is added afterwards at the
+// next segment's first limb by rp_ripple, in order, by wave 0, which then folds the carry
+// limb (value == f - top) as bp_canon does.  Returns the carry limb (1 only for 2^N) in
+// wave 0; scr: 2 NWV + 1 ints of LDS.
+template <int NWV>
+__device__ int rp_canon_par(const BSlot &b, int l, int wave, int lane, int *scr)
+{
+    const int rows = l >> 6, R = rows / NWV, u0 = wave * R;
+    int prevk = 0;
+    if (u0) {   // carry out of limb 64 u0 - 1 (f + c), read before any wave rewrites it
+        const u64 f = b.f[64 * u0 - 1];
+        const int c = b.c[64 * u0 - 1];
+        const u64 nf = f + (u64)(i64)c;
+        prevk = c >= 0 ? (int)(nf < f) : -(int)(nf > f);
+    }
+    __syncthreads();
+    u64 run1 = 0, run2 = 0;
+    int topk = 0;
+    for (int u = u0; u < u0 + R; ++u) {
+        const int m = 64 * u + lane;
+        const u64 f = b.f[m];
+        const int c = b.c[m];
+        u64 nf = f + (u64)(i64)c;
+        const int k = c >= 0 ? (int)(nf < f) : -(int)(nf > f);   // carry out of limb m, in {-1, 0, 1}
+        const int r = wv_ror1(k);
+        const int cm = lane ? r : prevk;                          // carry into limb m
+        prevk = wv_readlane(k, 63);
+        if (u == rows - 1) topk = prevk;                          // out of the top limb: the carry limb
+        const bool inc = cm == 1, dec = cm == -1;
+        {
+            const u64 X = __ballot(inc && nf == MPF_MAXL);
+            const u64 Yp = X | __ballot(inc ? nf == MPF_MAXL - 1 : nf == MPF_MAXL);
+            u64 s1, s2;
+            const bool o1 = add_ovf(X, Yp, &s1);
+            const bool o2 = add_ovf(s1, run1, &s2);
+            nf += (u64)inc + (((s2 ^ X ^ Yp) >> lane) & 1);
+            run1 = (o1 | o2) ? 1 : 0;
+        }
+        {
+            const u64 X = __ballot(dec && nf == 0);
+            const u64 Yp = X | __ballot(dec ? nf == 1 : nf == 0);
+            u64 s1, s2;
+            const bool o1 = add_ovf(X, Yp, &s1);
+            const bool o2 = add_ovf(s1, run2, &s2);
+            nf -= (u64)dec + (((s2 ^ X ^ Yp) >> lane) & 1);
+            run2 = (o1 | o2) ? 1 : 0;
+        }
+        b.f[m] = nf;
+    }
+    if (lane == 0) {
+        scr[2 * wave] = (int)run1;
+        scr[2 * wave + 1] = (int)run2;
+        if (wave == NWV - 1) scr[2 * NWV] = topk;
+    }
+    __syncthreads();
+    if (wave != 0) return 0;
+    int top = scr[2 * NWV] + scr[2 * (NWV - 1)] - scr[2 * (NWV - 1) + 1];
+    for (int w = 1; w < NWV; ++w) {   // run-outs of the lower segments (w - 1): almost never
+        const int d = scr[2 * (w - 1)] - scr[2 * (w - 1) + 1];
+        if (d > 0) top += rp_ripple(b, l, w * R, false, 1, lane);
+        if (d < 0) top -= rp_ripple(b, l, w * R, true, 1, lane);
+    }
+    if (top == 0) return 0;
+    // value == f - top, f in [0, 2^N), |top| <= 3: one ripple from limb 0, then the 2^N case
+    const bool sub = top > 0;
+    if (!rp_ripple(b, l, 0, sub, (u64)(sub ? top : -top), lane)) return 0;
+    // the ripple left 2^N: sub: f = 2^N + y - top >= 2^N - 3, true value f + 1;
+    // add: f = y + |top| - 2^N in {0, 1, 2}, true value f - 1
+    const u64 f0 = wv_readlane64(b.f[lane], 0);
+    const bool to_2N = sub ? (f0 == MPF_MAXL) : (f0 == 0);
+    if (to_2N) {
+        for (int u = 0; u < rows; ++u) b.f[64 * u + lane] = 0;
+        return 1;
+    }
+    if (lane == 0) b.f[0] = sub ? f0 + 1 : f0 - 1;
+    return 0;
+}
+
 // ---- scaling by 2^-(depth+1) and canonicalisation (mul_fft.c:3256-3260) ----------------
 // k_rscale<PP>: one coefficient per workgroup (many per CU, so one's load overlaps
 // another's arithmetic): load into the register pair form, multiply by 2^e with one general
 // rotation through LDS, then resolve every carry: the limbs go back to LDS in the k_bpass
-// slot form (limb + carry into it) and one wave sweeps the rows (bp_canon, the ballot
-// carry-lookahead of mpn_normmod_2expp1 :272) while the other waves wait; the canonical
-// residue in [0, 2^N] is stored with zero carry masks and its carry limb.
+// slot form (limb + carry into it) and the rows are swept (the ballot carry-lookahead of
+// mpn_normmod_2expp1 :272) by all eight waves, one segment each (rp_canon_par);
+// the canonical residue in [0, 2^N] is stored with zero carry masks and its carry limb.
 template <int PP>
 __global__ __launch_bounds__(RP_NT) void k_rscale(u64 *dig, u64 *cb, int *top, u32 N, u32 e)
 {
@@ -739,8 +853,8 @@ __global__ __launch_bounds__(RP_NT) void k_rscale(u64 *dig, u64 *cb, int *top, u
         *(short *)(b.c + 2 * pp) = (short)((pp ? hv : -hv) & 0xff);   // c_2pp = hin (|hin| < 128), c_2pp+1 = 0
     }
     __syncthreads();
-    if (t < 64) {
-        const int tv = bp_canon(b, l, t);
+    {
+        const int tv = rp_canon_par<RP_NT / 64>(b, l, t >> 6, t & 63, (int *)(smem + bp_slot_bytes(l) + (size_t)l));
         if (t == 0) SL[1] = (u32)tv;
     }
     __syncthreads();

@@ -10,6 +10,8 @@ SQ passes (each with GRBM_GUI_ACTIVE, so every ratio below uses the cycles of it
   valu_issue_util 2 * SQ_INSTS_VALU / (1024 SIMDs * cycles): a wave64 VALU op holds a SIMD-32
                   for 2 cycles (MI355X_MICROARCH.md "Wave scheduling"); multi-pass 64-bit ops
                   (v_mad_u64_u32, 64-bit shifts) make this a lower bound
+  valu_cycle_util_est  the same with SQ_INSTS_VALU_INT64 instructions at 8 cycles (v_mad_u64_u32
+                  is quarter rate: tests/microbench/mac_rate.hip) -- an upper estimate
   lds_util        SQ_LDS_IDX_ACTIVE / (256 CUs * cycles)
   wait_*_frac     SQ_WAIT_INST_ANY, SQ_WAIT_ANY over SQ_WAVE_CYCLES (quad-cycles both)
   waves_per_simd  4 * SQ_WAVE_CYCLES / (1024 * cycles): mean resident waves per SIMD
@@ -41,6 +43,9 @@ for k in sorted(set(f) | set(w) | set().union(*[set(s) for s in sq])):
                 rec[c] = v
         if "SQ_INSTS_VALU" in r:
             rec["valu_issue_util"] = 2 * r["SQ_INSTS_VALU"] / (1024 * cyc)
+            if "SQ_INSTS_VALU_INT64" in r:   # 64-bit integer ops (v_mad_u64_u32 ...) priced at 8 cycles
+                i64 = r["SQ_INSTS_VALU_INT64"]
+                rec["valu_cycle_util_est"] = (2 * (r["SQ_INSTS_VALU"] - i64) + 8 * i64) / (1024 * cyc)
         if "SQ_LDS_IDX_ACTIVE" in r:
             rec["lds_util"] = r["SQ_LDS_IDX_ACTIVE"] / (256 * cyc)
         if "SQ_WAVE_CYCLES" in r:

@@ -265,3 +265,97 @@ def test_mul_auto_exact_across_sizes(mp, oracle):
             b = mp.fill_random(n2, rng.getrandbits(64))
             got = mp.mul_auto(a, b)
             assert (got == oracle.gmp_mul(a, b)).all(), (n, n2, mp.choose(n, n2))
+
+
+def _reduced_pattern(kind, l, rng):
+    """(limbs, pos-carry limb set, neg-carry limb set, top) of a reduced-form residue built to
+    make the canonicalisation's carry chains long: through every limb, across the segment
+    boundaries of the multi-wave sweep, into and out of the carry limb."""
+    MAX = (1 << 64) - 1
+    if kind == 0:
+        return [MAX] * l, set(range(l)), set(), 0            # +1 into every limb: one chain through all
+    if kind == 1:
+        return [0] * l, set(), set(range(l)), 0              # -1 into every limb: borrows through all
+    if kind == 2:
+        return [MAX] * l, set(range(l)), set(), 1
+    if kind == 3:
+        return [0] * l, set(), set(range(l)), -1
+    if kind == 4:                                            # chains starting just below each segment boundary
+        limbs = [rng.getrandbits(64) for _ in range(l)]
+        pos = set()
+        for k in range(1, 8):
+            b = k * l // 8
+            for m in range(b - 3, b + 3):
+                limbs[m] = MAX
+            pos.add(b - 4)
+        return limbs, pos, set(), 0
+    if kind == 5:
+        limbs = [0] * l
+        neg = set()
+        for k in range(1, 8):
+            b = k * l // 8
+            neg.add(b - 4)
+        limbs[l - 1] = 0
+        return limbs, set(), neg, 2
+    if kind == 6:
+        return [MAX] * l, set(), set(), 0                    # 2^N - 1
+    if kind == 7:
+        return [0] * l, set(), set(), 1                      # 2^N
+    if kind == 8:
+        return [0] * l, {l - 1}, set(), 0                    # the top limb's carry: 2^N
+    limbs = [rng.getrandbits(64) for _ in range(l)]
+    ms = rng.sample(range(l), 40)
+    return limbs, set(ms[:20]), set(ms[20:]), rng.randint(-2, 2)
+
+
+@pytest.mark.parametrize("depth,w,nl", [(9, 128, 30000), (8, 512, 100000), (7, 2048, 150000)])
+def test_scale_canonicalisation_adversarial(mp, torch_dev, depth, w, nl):
+    """The scaling stage (x 2^-(depth+1), canonical store: k_rscale's multi-wave carry sweep at
+    l = 1024, 2048, 4096) on hand-made reduced-form residues whose carries ripple through every
+    limb, across the sweep's segment boundaries and through the carry limb, against exact
+    big-integer arithmetic (mpn_normmod_2expp1 / mpn_div_2expmod_2expp1 semantics,
+    mul_fft.c:272, :494, :3256-3260)."""
+    import torch
+    from gpu_stages import _cbs, _val
+    P = mp.plan_info(nl, nl, depth, w)
+    l, T, N = P["l"], P["trunc"], P["n"] * w
+    p = (1 << N) + 1
+    lay = mp.workspace_layout(nl, nl, depth, w)
+    ws = mp.alloc_workspace(nl, nl, depth, w, torch_dev)
+    ws.fill_(0)
+    digA, topA, _, _ = mp.workspace_views(ws, nl, nl, depth, w)
+    cbw = lay["cbw"]
+    rng = random.Random(depth * 31 + w)
+    dig = np.zeros((T, l), np.uint64)
+    top = np.zeros(T, np.int32)
+    cbm = np.zeros((T, cbw), np.uint64)
+    want = []
+    for sl in range(T):
+        limbs, pos, neg, t = _reduced_pattern(sl % 10, l, rng)
+        dig[sl] = np.array(limbs, dtype=np.uint64)
+        top[sl] = t
+        v = sum(x << (64 * m) for m, x in enumerate(limbs)) + t * (1 << N)
+        for m in pos:
+            cbm[sl, 2 * (m // 64)] |= np.uint64(1 << (m % 64))
+            v += 1 << (64 * (m + 1))
+        for m in neg:
+            cbm[sl, 2 * (m // 64) + 1] |= np.uint64(1 << (m % 64))
+            v -= 1 << (64 * (m + 1))
+        want.append(v * pow(2, 2 * N - depth - 1, p) % p)
+    digA[:T] = torch.from_numpy(dig.view(np.int64)).to(torch_dev)
+    topA[:T] = torch.from_numpy(top).to(torch_dev)
+    u8 = ws.view(torch.uint8)
+    u8[lay["cbA"]: lay["cbA"] + T * cbw * 8] = torch.from_numpy(cbm.view(np.uint8).reshape(-1)).to(torch_dev)
+    z = torch.zeros(1, dtype=torch.int64, device=torch_dev)
+    mp.stage(mp.STAGE_SCALE, z, z, z, nl, nl, depth, w, ws)
+    torch.cuda.synchronize()
+    gd = digA.cpu().numpy().view(np.uint64)
+    gt = topA.cpu().numpy().astype(np.int64)
+    gc = _cbs(mp, ws, nl, nl, depth, w, 0)
+    bad = []
+    for sl in range(T):
+        v = _val(gd, gt, sl, N)
+        canon = not gc[sl].any() and (gt[sl] == 0 or (gt[sl] == 1 and not gd[sl].any()))
+        if not canon or v != want[sl]:
+            bad.append(sl)
+    assert not bad, f"{len(bad)} of {T} slots wrong or not canonical, first {bad[:8]}"
