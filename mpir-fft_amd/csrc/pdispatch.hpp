@@ -10,6 +10,9 @@ typedef void (*pw_fn)(uint64_t *, uint64_t *, int *, const uint64_t *, const uin
 // level fused into the load, product to the C arrays), nullptr if not built
 pw_fn pw_get(int M, int lk, int fuse = 0);
 size_t pw_lds(int M, int K, int l);
+// k_pw2<M, lk, fuse>: the same with two threads per piece (p2kernels.hpp; 2^(lk+1) threads)
+pw_fn pw2_get(int M, int lk, int fuse = 0);
+size_t pw2_lds(int M, int K, int l);
 
 // Inner ring for a product mod 2^(64 l) + 1 cut into K = 2^lk pieces: the smallest M
 // (limbs) with 64 M >= 2 (64 l / K) + lk + 2 and 64 M a multiple of K (theta = 2^(64 M / K)).

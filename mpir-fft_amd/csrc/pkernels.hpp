@@ -450,8 +450,9 @@ __device__ __forceinline__ void pw_slot_product(u64 (&La)[M], int Ta, u64 (&Lb)[
 
 // R = sum_t c_t 2^(B t) mod 2^N + 1 from X / TT, stored in the reduced HBM form at
 // (pa, cbp, *topp).  c_t 2^(Bt) = v_t 2^(Bt) - s_t (2^(Bt) + 2^(N' + Bt)); positions >= N
-// wrap negated.  Thread t sums output limbs m = t + K r (coalesced, consecutive per wave).
-template <int M, int LK>
+// wrap negated.  Thread t of NTH sums output limbs m = t + NTH r (coalesced, consecutive
+// per wave).
+template <int M, int LK, int NTH = (1 << LK)>
 __device__ __forceinline__ void pw_slot_output(const u64 *X, const int *TT, int *H, u64 *pa, u64 *cbp, int *topp, int l,
                                                int t)
 {
@@ -460,13 +461,13 @@ __device__ __forceinline__ void pw_slot_output(const u64 *X, const int *TT, int 
     const int lane = t & 63;
     u64 fo[8];
     int ho[8];
-    const int RPT = l / K;   // <= 8 (host)
+    const int RPT = l / NTH;   // <= 8 (host)
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
         fo[r] = 0;
         ho[r] = 0;
         if (r >= RPT) continue;
-        const int m = t + K * r;
+        const int m = t + NTH * r;
         i128 S = 0;
         // pieces whose limbs [t'LP, t'LP + M] cover m, directly and through the wrap (m + l)
 #pragma unroll
@@ -493,7 +494,7 @@ __device__ __forceinline__ void pw_slot_output(const u64 *X, const int *TT, int 
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
         if (r >= RPT) continue;
-        const int m = t + K * r;
+        const int m = t + NTH * r;
         const int hin = m ? H[m - 1] : -H[l - 1];
         const u64 f = fo[r];
         const u64 nf = f + (u64)(i64)hin;

@@ -1,15 +1,35 @@
 #!/bin/bash
-# Limiter counters of the C3 kernels, the pointwise k_pwss first:
-# counter list, then two SQ passes with GRBM_GUI_ACTIVE each (durations from a kernel-trace
-# pass of the same command; clocks only ever derived inside one pass).
-cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out && \
-B="python3 bench.py --config ${CFG:-C3} --steps 1 --warmup 0 --no-cpu-baseline --no-check --e2e-reps 0" && \
-(timeout -s KILL 60 rocprofv3 -L > gpurun_out/counters_list.txt 2>&1 || true) && \
-timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_sqa -o c -- $B > gpurun_out/pmc_sqa.log 2>&1 && \
-timeout -s KILL 150 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_sqb -o c -- $B > gpurun_out/pmc_sqb.log 2>&1 && \
-timeout -s KILL 150 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pmc_kt -o c -- $B > gpurun_out/pmc_kt.log 2>&1
-rc=$?; echo "rc=$rc"
-python3 scripts/pmc_summary.py gpurun_out/pmc_sqa gpurun_out/pmc_sqa.json > /dev/null 2>&1
-python3 scripts/pmc_summary.py gpurun_out/pmc_sqb gpurun_out/pmc_sqb.json > /dev/null 2>&1
-grep -i -E "^(SQ_|GRBM_)|SQ_ACTIVE|SQ_WAIT|LDS" gpurun_out/counters_list.txt | head -80
-exit $rc
+# SQ limiter counters of the pointwise stage alone (scripts/pw_time.py) per MPFFT_POINTWISE kind.
+# usage: scripts/gpu_pmc_pw.sh C3 "pwss pwss2"
+cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out || exit 1
+CFG=${1:-C3}
+for k in ${2:-pwss pwss2}; do
+  for P in "sqa:SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE" \
+           "sqb:SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VALU_INT64 SQ_INSTS_VALU GRBM_GUI_ACTIVE"; do
+    t=${P%%:*}; c=${P#*:}; d=gpurun_out/pmcpw_${CFG}_${k}_$t
+    MPFFT_POINTWISE=$k timeout -s KILL 90 rocprofv3 --pmc $c --output-format csv -d $d -o c -- python3 scripts/pw_time.py $CFG 1 > $d.log 2>&1 || exit 1
+    python3 scripts/pmc_summary.py $d $d.json > /dev/null || exit 1
+  done
+done
+python3 - "$CFG" ${2:-pwss pwss2} <<'PY'
+import json, sys, glob
+cfg = sys.argv[1]
+for k in sys.argv[2:]:
+    m = {}
+    for t in ("sqa", "sqb"):
+        for name, v in json.load(open(f"gpurun_out/pmcpw_{cfg}_{k}_{t}.json")).items():
+            if "k_pw" in name:
+                m.setdefault(name[:24], {}).update(v)
+    for name, v in m.items():
+        cyc = v["GRBM_GUI_ACTIVE"] / 8
+        print(k, name, {a: round(b) for a, b in sorted(v.items())})
+        # the formulas of scripts/pmc_merge.py
+        print("   valu_issue", round(2 * v["SQ_INSTS_VALU"] / (1024 * cyc), 3),
+              "valu_cyc_est", round((2 * (v["SQ_INSTS_VALU"] - v["SQ_INSTS_VALU_INT64"]) + 8 * v["SQ_INSTS_VALU_INT64"]) / (1024 * cyc), 3),
+              "lds_util", round(v["SQ_LDS_IDX_ACTIVE"] / (256 * cyc), 3),
+              "waves/simd", round(4 * v["SQ_WAVE_CYCLES"] / (1024 * cyc), 2),
+              "wait_inst", round(v["SQ_WAIT_INST_ANY"] / v["SQ_WAVE_CYCLES"], 3),
+              "wait_any", round(v["SQ_WAIT_ANY"] / v["SQ_WAVE_CYCLES"], 3),
+              "bank_conf/idx", round(v["SQ_LDS_BANK_CONFLICT"] / max(1, v["SQ_LDS_IDX_ACTIVE"]), 3),
+              "dur_ms", round(v["duration_ns"] / 1e6, 3))
+PY
