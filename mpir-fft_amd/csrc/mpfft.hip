@@ -93,16 +93,14 @@ static int ilog2(long v) { int d = 0; while ((1L << d) < v) ++d; return d; }
 
 // pointwise kernel family.  MPFFT_POINTWISE is the one runtime selector the shipped library
 // reads (every choice is an exact product; the parity tests A/B them): auto (default),
-// pwss = the nested negacyclic k_pwss (l = 1024, 2048, 4096), pwss2 = the same with two
-// threads per piece (k_pw2, p2kernels.hpp), mfma = int8-MFMA k_pwm2 (l % 256 == 0),
-// mfma1 = k_pwm (l % 128 == 0), valu = k_pw.
-enum { PW_AUTO = 0, PW_PWSS, PW_PWSS2, PW_MFMA, PW_MFMA1, PW_VALU };
+// pwss = the nested negacyclic k_pwss (l = 1024, 2048, 4096), mfma = int8-MFMA k_pwm2
+// (l % 256 == 0), mfma1 = k_pwm (l % 128 == 0), valu = k_pw.
+enum { PW_AUTO = 0, PW_PWSS, PW_MFMA, PW_MFMA1, PW_VALU };
 static int pw_kind()
 {
     const char *e = getenv("MPFFT_POINTWISE");
     if (!e) return PW_AUTO;
     if (!strcmp(e, "pwss")) return PW_PWSS;
-    if (!strcmp(e, "pwss2")) return PW_PWSS2;
     if (!strcmp(e, "mfma")) return PW_MFMA;
     if (!strcmp(e, "mfma1")) return PW_MFMA1;
     if (!strcmp(e, "valu")) return PW_VALU;
@@ -114,7 +112,7 @@ static int pw_kind()
 static int pwss_lk_of(long l)
 {
     const int k = pw_kind();
-    if (k != PW_AUTO && k != PW_PWSS && k != PW_PWSS2) return 0;
+    if (k != PW_AUTO && k != PW_PWSS) return 0;
     switch (l) {
     case 1024: return k != PW_AUTO ? 8 : 0;
     case 2048: return 8;
@@ -123,15 +121,11 @@ static int pwss_lk_of(long l)
     return 0;
 }
 
-// the nested negacyclic kernel the selector names: k_pw2 (two threads per piece) or k_pwss
-static bool pw_two() { return pw_kind() == PW_PWSS2; }
-static pw_fn pw_pick(int M, int lk, int fuse = 0) { return pw_two() ? pw2_get(M, lk, fuse) : pw_get(M, lk, fuse); }
-
 // the fused-pair k_pwss instance (last row DIF level on load, product to C) exists for l
 static bool pw_pair_kernel(long l)
 {
     const int lk = pwss_lk_of(l);
-    return lk && pw_pick(pw_inner_limbs(l, lk), lk, 1) != nullptr;
+    return lk && pw_get(pw_inner_limbs(l, lk), lk, 1) != nullptr;
 }
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -642,7 +636,7 @@ struct Exec {
     bool pwss_active() const
     {
         const int lk = pwss_lk(P.l);
-        return lk && pw_pick(pw_inner_limbs(P.l, lk), lk) != nullptr;
+        return lk && pw_get(pw_inner_limbs(P.l, lk), lk) != nullptr;
     }
 
     int pointwise()
@@ -652,10 +646,9 @@ struct Exec {
         if (const int lk = pwss_lk(P.l)) {
             const int M = pw_inner_limbs(P.l, lk);
             const bool pair = row_fused();
-            pw_fn f = pw_pick(M, lk, pair ? 1 : 0);
+            pw_fn f = pw_get(M, lk, pair ? 1 : 0);
             if (f) {
-                const bool two = pw_two();
-                const size_t lds = two ? pw2_lds(M, 1 << lk, (int)P.l) : pw_lds(M, 1 << lk, (int)P.l);
+                const size_t lds = pw_lds(M, 1 << lk, (int)P.l);
                 allow_lds((const void *)f, lds);
                 static const bool stamps = diag_env("MPFFT_PW_STAMPS") != nullptr;
                 unsigned long long *dbg = nullptr;
@@ -663,7 +656,7 @@ struct Exec {
                     HIPCHK(hipMalloc((void **)&dbg, (size_t)cnt * 64));
                     HIPCHK(hipMemsetAsync(dbg, 0, (size_t)cnt * 64, s));
                 }
-                hipLaunchKernelGGL(f, dim3((unsigned)cnt), dim3((two ? 2u : 1u) << lk), lds, s, row.dig[0], row.cb[0], row.top[0],
+                hipLaunchKernelGGL(f, dim3((unsigned)cnt), dim3(1u << lk), lds, s, row.dig[0], row.cb[0], row.top[0],
                                    (const u64 *)row.dig[1], (const u64 *)row.cb[1], (const int *)row.top[1], (int)P.l,
                                    cview.dig[0], cview.cb[0], cview.top[0], dbg);
                 HIPCHK(hipGetLastError());
@@ -1160,11 +1153,11 @@ int mpfft_stage_kernels(long n1, long n2, unsigned long depth, unsigned long w, 
     const char *pass = P.big ? (P.rpass ? "k_rpass" : "k_bpass") : (P.wave && P.lds) ? "k_lpass" : P.wave ? "k_wpass" : "k_pass";
     char pw[64];
     const int lk = Exec::pwss_lk(P.l);
-    const char *rows = P.big && P.rpass && !(lk && pw_pick(pw_inner_limbs(P.l, lk), lk)) ? "k_rpass + k_bpass (canonical last pass)" : pass;
+    const char *rows = P.big && P.rpass && !(lk && pw_get(pw_inner_limbs(P.l, lk), lk)) ? "k_rpass + k_bpass (canonical last pass)" : pass;
     const char *fz = diag_env("MPFFT_FUSE_ROW");
     const bool fused = P.has_c && !(fz && !strcmp(fz, "0"));   // as Exec::row_fused() in run_all
-    if (lk && pw_pick(pw_inner_limbs(P.l, lk), lk))
-        snprintf(pw, sizeof pw, "%s<%d>%s (nested negacyclic, K=%d)", pw_two() ? "k_pw2" : "k_pwss", pw_inner_limbs(P.l, lk),
+    if (lk && pw_get(pw_inner_limbs(P.l, lk), lk))
+        snprintf(pw, sizeof pw, "k_pwss<%d>%s (nested negacyclic, K=%d)", pw_inner_limbs(P.l, lk),
                  fused ? " pair + last row level" : "", 1 << lk);
     else if (P.l % 256 == 0 && P.l <= 4096 && pw_kind() != PW_MFMA1 && pw_kind() != PW_VALU)
         snprintf(pw, sizeof pw, "k_pwm2 (int8 MFMA)");

@@ -6,12 +6,18 @@
 //   * a, b are cut into K = 2^lk pieces of B = N/K bits (thread t owns piece t);
 //   * the negacyclic convolution of the pieces (X^K == -1 with X = 2^B, so it IS the
 //     product mod p) is computed in the inner ring R' = Z/(2^N' + 1), N' = 64 M, with
-//     N' >= 2B + lk + 2 so every signed convolution coefficient |c_t| < K 2^(2B) is
+//     N' >= 2B + lk + 4 so every signed convolution coefficient |c_t| < K 2^(2B+2) is
 //     recovered exactly from its residue (the reference instead restores the top
 //     with a naive convolution of the low limbs, :3088; headroom is cheaper here);
-//   * negacyclic weights theta^t = 2^(t N'/K), then a length-K cyclic DIF transform
-//     with root omega = theta^2, pointwise products in R', DIT inverse, division by
-//     K and un-weighting -- all multiplications by powers of two.
+//   * negacyclic weights theta^t, theta = 2^(N'/K) a 2K-th root of unity, then a length-K
+//     cyclic DIF transform with root omega = theta^2 = 2^(2N'/K), pointwise products in R',
+//     DIT inverse, division by K and un-weighting.  Only omega must be a power of two:
+//     N' is a multiple of K/2 (not K), and when N'/K is a half-integer the odd weights use
+//     sqrt(2) = 2^(N'/4) (2^(N'/2) - 1) in R' (pw_sqrt2, one in-thread half swap) -- the
+//     identity of the reference's FFT_radix2_butterfly_sqrt2 (mul_fft.c:580-640) applied to the inner
+//     ring.  That lets N' be the smallest multiple of 64 K/2 bits above the headroom bound
+//     (C3: 1152 instead of 1280 bits, C4: 1280 instead of 1536).
+//   All the other multiplications are by powers of two.
 // Thread t holds its coefficient (M limbs + a small signed top word, value =
 // limbs + top 2^N') in registers: additions are in-thread carry chains
 // (v_add_co / v_addc).  A butterfly partner is read from LDS (limb-major,
@@ -175,6 +181,36 @@ __host__ __device__ __forceinline__ int pw_canon(u64 (&L)[M], int T)
     return 0;
 }
 
+// L + T 2^N'  <-  (2^(N'/2) - 1) (L + T 2^N')  mod p'  (M even; lo, hi = the low and high
+// M/2 limbs of L):  2^(N'/2) (lo + hi 2^(N'/2) + T 2^N') == lo 2^(N'/2) - hi - T 2^(N'/2), so
+// the product is (T - hi - lo) + (lo - hi - T) 2^(N'/2): two interleaved chains, then the low
+// chain's carry (in [-2, 1]) rippled into the high half.  The new top is small (|T'| <= |T| + 3).
+template <int M>
+__host__ __device__ __forceinline__ void pw_sqrt2(u64 (&L)[M], int &T)
+{
+    static_assert(M % 2 == 0, "the half swap needs an even limb count");
+    constexpr int H = M / 2;
+    i128 a0 = (i128)T, a1 = -(i128)T;
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        const u64 lo = L[j], hi = L[j + H];
+        a0 += -(i128)hi - (i128)lo;
+        a1 += (i128)lo - (i128)hi;
+        L[j] = (u64)a0;
+        L[j + H] = (u64)a1;
+        a0 >>= 64;
+        a1 >>= 64;
+    }
+    i128 c = a0;
+#pragma unroll
+    for (int j = H; j < M; ++j) {
+        c += (i128)L[j];
+        L[j] = (u64)c;
+        c >>= 64;
+    }
+    T = (int)(i64)(a1 + c);
+}
+
 // z = a b mod p' for canonical a (La, ta), b (Lb, tb); result limbs + top (value = L + T 2^N')
 template <int M>
 __host__ __device__ __forceinline__ void pw_mulmod(u64 (&Z)[M], int &T, const u64 (&La)[M], int ta, const u64 (&Lb)[M],
@@ -266,7 +302,7 @@ __device__ __forceinline__ void pw_publish(u64 (&L)[M], int &T, int S, u32 *Xw, 
     TT[t] = 2 * T + S;
 }
 
-// One forward (DIF) or inverse (DIT) length-K cyclic transform with root 2^(2 TH) over
+// One forward (DIF) or inverse (DIT) length-K cyclic transform with root 2^W2 over
 // the values of the K threads of this workgroup.  P: this thread's pending exponent.
 // a mod n for a < 4n, without a division (every exponent here is a sum of a few reduced terms)
 __device__ __forceinline__ unsigned pw_mod(unsigned a, unsigned n)
@@ -288,19 +324,18 @@ __device__ __forceinline__ void pw_wave_sync()
 
 template <int M, int LK, int DIR>
 __device__ __forceinline__ void pw_transform(u64 (&L)[M], int &T, int &S, unsigned &P, u32 *Xw, int *TT, unsigned *PP,
-                                             unsigned TH, int t)
+                                             unsigned W2, int t)
 {
     constexpr int K = 1 << LK, lk = LK;
     constexpr unsigned N2 = 128 * M;
-    // the level twiddle unit (2 TH) << j, reduced once per level; tw = (qt mod h) * unit < 2N' * ...
     for (int jj = 0; jj < lk; ++jj) {
         const int j = DIR == 0 ? jj : lk - 1 - jj;   // DIF level index (DIT runs them backwards)
         const int h = K >> (j + 1);
         const int q = t ^ h;
         const bool top = !(t & h);
         const int qt = t & ~h;                       // top index of the pair
-        // (qt mod h) 2^j < K/2, times 2 TH: below N' (= K TH): no reduction needed
-        const unsigned tw = (unsigned)((qt & (h - 1)) << j) * (2 * TH);
+        // (qt mod h) 2^j < K/2, times W2: below N' (= K W2 / 2): no reduction needed
+        const unsigned tw = (unsigned)((qt & (h - 1)) << j) * W2;
         const bool cross = h >= 64;                  // partner in another wave
         pw_publish<M, LK>(L, T, S, Xw, TT, t);
         PP[t] = P;
@@ -329,7 +364,7 @@ __device__ __forceinline__ void pw_transform(u64 (&L)[M], int &T, int &S, unsign
 // and minus the carry limb (both weigh 2^N == -1); the carry out of the piece's top limb
 // is the next piece's.  The value v (-2 <= v < 2^(64 LP) + 2^(64 LP - 64)) is returned as
 // L + T 2^N', T in {-1, 0}: the convolution tolerates such pieces (|c_t| < K 2^(2B+1)
-// still fits the headroom N' >= 2B + lk + 2), so the pointwise inputs need no
+// still fits the headroom N' >= 2B + lk + 4, pdispatch.hpp), so the pointwise inputs need no
 // canonicalisation pass.  A piece lies inside one 64-limb mask row (LP | 64).
 template <int M, int LP>
 __device__ __forceinline__ void pw_load_piece(u64 (&L)[M], int &T, const u64 *dig, const u64 *cbp, int top, int l, int t)
@@ -362,14 +397,15 @@ __device__ __forceinline__ void pw_load_piece(u64 (&L)[M], int &T, const u64 *di
     T = c < 0 ? -1 : 0;
 }
 
-// limbs per piece of the instantiated k_pwss shapes: l / K (l = 1024, 2048, 4096)
+// limbs per piece of the instantiated k_pwss shapes: l / K (l = 1024: M = 10, LP = 4;
+// l = 2048, 4096: M = 18, 20, LP = 8)
 template <int M, int LK>
-__host__ __device__ constexpr int pw_piece_limbs() { return M == 12 ? 4 : 8; }
+__host__ __device__ constexpr int pw_piece_limbs() { return M <= 12 ? 4 : 8; }
 
 // Piece t of x0 + x1 (sub = 0) or x0 - x1 (sub = 1) for two reduced-form coefficients: the
 // last DIF level of the row transform (h = 1, twiddle 1) applied piecewise -- linear, so the
 // pieces of the sum / difference are the sums / differences of the pieces (|c_t| at most
-// doubles: far inside the headroom N' >= 2B + lk + 2).  Each piece is LP limbs plus a carry
+// doubles: the headroom N' >= 2B + lk + 4 covers it, pdispatch.hpp).  Each piece is LP limbs plus a carry
 // in {-1, 0, 1} (pw_load_piece); the LP + 1 limb result is sign-extended to M limbs, T = -1
 // for a negative value.
 template <int M, int LP>
@@ -408,13 +444,21 @@ __device__ __forceinline__ void pw_slot_product(u64 (&La)[M], int Ta, u64 (&Lb)[
 #define PW_STAMP(k) do { if (stamp && t == 0) stamp[k] = __builtin_amdgcn_s_memtime(); } while (0)
     constexpr int K = 1 << LK, lk = LK;
     constexpr unsigned NP = 64 * M, N2 = 2 * NP;
-    const unsigned TH = NP >> lk;                // theta = 2^TH
+    constexpr unsigned W2 = N2 >> lk;            // omega = 2^W2 (host: K / 2 divides N')
+    static_assert((N2 >> lk) << lk == N2, "omega must be a power of two");
     int Sa = 0, Sb = 0;                          // sign flags
-    unsigned Pa = (unsigned)t * TH, Pb = Pa;     // negacyclic weight theta^t (t TH < N')
+    // negacyclic weight theta^t = 2^(t W2 / 2); a half-integer exponent (W2 and t odd) is
+    // 2^(floor(t W2 / 2) + N'/4) (2^(N'/2) - 1)  (sqrt 2 = 2^(N'/4) (2^(N'/2) - 1) in R')
+    const bool half = (W2 & 1) && (t & 1);
+    unsigned Pa = (((unsigned)t * W2) >> 1) + (half ? NP / 4 : 0), Pb = Pa;   // < N' + N'/4
+    if (half) {
+        pw_sqrt2<M>(La, Ta);
+        pw_sqrt2<M>(Lb, Tb);
+    }
     PW_STAMP(1);
-    pw_transform<M, LK, 0>(La, Ta, Sa, Pa, Xw, TT, PP, TH, t);
+    pw_transform<M, LK, 0>(La, Ta, Sa, Pa, Xw, TT, PP, W2, t);
     PW_STAMP(2);
-    pw_transform<M, LK, 0>(Lb, Tb, Sb, Pb, Xw, TT, PP, TH, t);
+    pw_transform<M, LK, 0>(Lb, Tb, Sb, Pb, Xw, TT, PP, W2, t);
     PW_STAMP(3);
 
     // ---- inner products: 2^Pa xa * 2^Pb xb = 2^(Pa + Pb) (xa xb) ---------------------
@@ -426,11 +470,14 @@ __device__ __forceinline__ void pw_slot_product(u64 (&La)[M], int Ta, u64 (&Lb)[
     PW_STAMP(4);
 
     // ---- inverse, then 2^-lk (division by K) and theta^-t --------------------------
-    pw_transform<M, LK, 1>(Z, Tz, Sz, Pz, Xw, TT, PP, TH, t);
+    pw_transform<M, LK, 1>(Z, Tz, Sz, Pz, Xw, TT, PP, W2, t);
     PW_STAMP(5);
     {
-        const unsigned un = (unsigned)t * TH + lk;   // < N' + lk
-        const unsigned F = pw_mod(Pz + N2 - un, N2);
+        // theta^-t 2^-lk: 2^-(t W2 / 2 + lk), for a half-integer t W2 / 2 (sqrt 2)^-1 = sqrt 2 / 2:
+        // 2^(-floor(t W2 / 2) - 1 - lk + N'/4) (2^(N'/2) - 1)
+        const unsigned un = (((unsigned)t * W2) >> 1) + lk + (half ? 1 : 0);   // < N' + lk + 1
+        const unsigned F = pw_mod(Pz + N2 - un + (half ? NP / 4 : 0), N2);
+        if (half) pw_sqrt2<M>(Z, Tz);
         pw_publish<M, LK>(Z, Tz, Sz, Xw, TT, t);
         pw_wave_sync();                                  // own column only
         pw_combine<M, LK>(Z, Tz, Sz, 0, Xw, TT, t, F);   // clears the sign flag

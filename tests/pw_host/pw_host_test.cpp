@@ -64,12 +64,34 @@ template <int M> int run() {
         if (mpz_cmp(got, want)) { if (bad++ < 5) printf("canon mismatch it=%d\n", it); }
     }
     printf("M=%d mulmod/canon bad=%d\n", M, bad);
-    return bad + bad0;
+    int bad1 = bad;
+    bad = 0;
+    // pw_sqrt2: (2^(N'/2) - 1) x, and its square 2^(N'/2) (2^(N'/2) - 1)^2 == 2 (the sqrt 2
+    // identity the odd negacyclic weights rely on, mul_fft.c:579-640)
+    mpz_t h; mpz_init(h);
+    for (int it = 0; it < 20000; ++it) {
+        u64 L[M]; int T = (int)(rng() % 9) - 4;
+        for (int j = 0; j < M; ++j) L[j] = it % 9 == 4 ? (it % 2 ? ~0ull : 0ull) : rng();
+        tovals<M>(a, L, T);
+        mpz_set_ui(h, 1); mpz_mul_2exp(h, h, 32 * M); mpz_sub_ui(h, h, 1);
+        mpz_mul(want, a, h); mpz_mod(want, want, p);
+        pw_sqrt2<M>(L, T);
+        tovals<M>(got, L, T); mpz_mod(got, got, p);
+        if (mpz_cmp(got, want)) { if (bad++ < 5) printf("sqrt2 mismatch it=%d\n", it); }
+        if (T < -8 || T > 8) { if (bad++ < 5) printf("sqrt2 top out of range T=%d\n", T); }
+        if (it == 0) {   // 2^(N'/4) (2^(N'/2) - 1) squared is 2
+            mpz_set_ui(a, 1); mpz_mul_2exp(a, a, 16 * M); mpz_mul(a, a, h); mpz_mul(a, a, a); mpz_mod(a, a, p);
+            if (mpz_cmp_ui(a, 2)) { ++bad; printf("sqrt2 identity fails\n"); }
+        }
+    }
+    mpz_clear(h);
+    printf("M=%d sqrt2 bad=%d\n", M, bad);
+    return bad + bad0 + bad1;
 }
 
 int main()
 {
-    int bad = run<12>() + run<20>() + run<24>();
+    int bad = run<10>() + run<18>() + run<20>();
     printf(bad ? "FAIL\n" : "OK\n");
     return bad != 0;
 }

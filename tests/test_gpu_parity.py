@@ -116,8 +116,7 @@ def _pattern(kind, l, N, rng):
 
 PW_CASES = [(k, d, w) for k in ("mfma", "mfma1", "valu")
             for d, w in ((11, 1), (9, 16), (8, 64), (7, 256), (6, 1024), (5, 4096), (6, 4096))] + \
-           [(k, d, w) for k in ("pwss", "pwss2") for d, w in ((6, 1024), (5, 4096), (6, 4096))] + \
-           [("auto", 5, 4096), ("auto", 6, 4096)]
+           [("pwss", 6, 1024), ("pwss", 5, 4096), ("pwss", 6, 4096), ("auto", 5, 4096), ("auto", 6, 4096)]
 
 
 @pytest.mark.parametrize("kind,depth,w", PW_CASES)
@@ -127,8 +126,7 @@ def test_pointwise_direct(mp, torch_dev, kind, depth, w):
     kernel family MPFFT_POINTWISE selects: the int8-MFMA kernels (mfma: k_pwm2 when
     l % 256 == 0; mfma1: k_pwm), the VALU schoolbook (valu: k_pw) and the nested
     negacyclic k_pwss (pwss: l = 1024, 2048, 4096 -- the default from l = 2048 on,
-    "auto") and its two-threads-per-piece form k_pw2 (pwss2).  The kernel that ran is
-    checked through mpfft_stage_kernels."""
+    "auto").  The kernel that ran is checked through mpfft_stage_kernels."""
     import torch
     from gpu_stages import _cbs, _val_reduced
     mx = max_limbs(depth, w)
@@ -163,7 +161,7 @@ def test_pointwise_direct(mp, torch_dev, kind, depth, w):
     try:
         ran = mp.stage_kernels(n1, n2, depth, w)["pointwise"].split(" ")[0].split("<")[0]
         mfma1 = "k_pwm" if l % 128 == 0 else "k_pw"
-        expect = {"pwss": "k_pwss", "pwss2": "k_pw2", "auto": "k_pwss", "valu": "k_pw", "mfma1": mfma1,
+        expect = {"pwss": "k_pwss", "auto": "k_pwss", "valu": "k_pw", "mfma1": mfma1,
                   "mfma": "k_pwm2" if l % 256 == 0 else mfma1}[kind]
         assert ran == expect, (kind, l, ran)
         mp.stage(mp.STAGE_POINTWISE, da, db, dr, n1, n2, depth, w, ws)
@@ -257,19 +255,18 @@ def test_c2_c3_exact_vs_gmp(mp, oracle):
         assert (got == oracle.gmp_mul(a, b)).all()
 
 
-@pytest.mark.parametrize("kind", ["pwss", "pwss2"])
-def test_nested_pointwise_full_products(mp, oracle, kind):
-    """Whole products through each nested negacyclic kernel (k_pwss, k_pw2) at l = 1024,
-    2048 (the C2 shape: fused pair + last row level) and 4096, against GMP mpn_mul."""
+def test_nested_pointwise_full_products(mp, oracle):
+    """Whole products through k_pwss at l = 1024, 2048 (the C2 shape: fused pair + last
+    row level) and 4096 (fused pair), against GMP mpn_mul."""
     old = os.environ.get("MPFFT_POINTWISE")
-    os.environ["MPFFT_POINTWISE"] = kind
+    os.environ["MPFFT_POINTWISE"] = "pwss"
     try:
         for depth, w, nl in ((6, 1024, 32760), (7, 1024, 131064), (15, 4, 15625000), (6, 4096, 131064)):
             ran = mp.stage_kernels(nl, nl, depth, w)["pointwise"]
-            assert ran.startswith("k_pw2<" if kind == "pwss2" else "k_pwss<"), ran
+            assert ran.startswith("k_pwss<"), ran
             a = mp.fill_random(nl, 0x3003 + depth)
             b = mp.fill_random(nl - 17, 0x4004 + w)
-            assert (mp.mul(a, b, depth, w) == oracle.gmp_mul(a, b)).all(), (kind, depth, w, ran)
+            assert (mp.mul(a, b, depth, w) == oracle.gmp_mul(a, b)).all(), (depth, w, ran)
     finally:
         if old is None:
             os.environ.pop("MPFFT_POINTWISE", None)

@@ -1,7 +1,7 @@
 """CPU test: the nested negacyclic pointwise arithmetic of k_pwss (pkernels.hpp) --
-rotated add in Z/(2^N'+1), inner product, canonical residue -- compiled for the host
-and checked against GMP (tests/pw_host/pw_host_test.cpp), for every inner size the
-library instantiates (M = 12, 20, 24 limbs).  Reference algorithm: FFT_mulmod_2expp1
+rotated add in Z/(2^N'+1), inner product, canonical residue and the sqrt 2 weight step
+(pw_sqrt2) -- compiled for the host and checked against GMP (tests/pw_host/pw_host_test.cpp),
+for every inner size the library instantiates (M = 10, 18, 20 limbs).  Reference algorithm: FFT_mulmod_2expp1
 (/root/reference/mul_fft.c:2998-3117), whose test oracle is mpn_mulmod_2expp1 (:4224)."""
 import os
 import subprocess
