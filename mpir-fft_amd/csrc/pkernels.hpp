@@ -29,11 +29,21 @@
 #pragma once
 #include "coeff.hpp"
 
-// LDS of one k_pwss workgroup: (M + 1) K limbs + tops + pending exponents + l overflows
+// LDS of one k_pwss workgroup: M K limbs (the exchange rows, then the coefficients; the l
+// output overflows alias them) + tops + pending exponents.  C3 (M = 18, K = 256): 38 912 B,
+// so four workgroups share a CU's 160 KiB (pw_wpe).
 __host__ __device__ constexpr size_t pw_lds_bytes(int M, int K, int l)
 {
-    return (size_t)(M + 1) * K * 8 + (size_t)K * 8 + (size_t)l * 4;
+    return ((size_t)M * K * 8 > (size_t)l * 4 ? (size_t)M * K * 8 : (size_t)l * 4) + (size_t)K * 8;
 }
+
+// waves per SIMD k_pwss is compiled for: 4 (VGPRs <= 128) where four workgroups fit the LDS
+// (K = 256: 1024 threads per CU), else 2 (the compiler's choice, ~140-170 VGPRs)
+template <int M, int LK>
+__host__ __device__ constexpr int pw_wpe() { return LK == 8 && pw_lds_bytes(M, 1 << LK, 64 * M) * 4 <= 160 * 1024 ? 4 : 2; }
+// partner-word prefetch distance of pw_combine for that budget
+template <int M, int LK>
+__host__ __device__ constexpr int pw_pd() { return pw_wpe<M, LK>() == 4 ? 16 : 2 * M; }
 
 // Exchange format: thread t publishes its value as 2M 32-bit words, word k at
 // Xw[k K + t] (conflict-free for any rotation), top in TT[t].  Before publishing,
@@ -83,7 +93,7 @@ __host__ __device__ __forceinline__ int pw_norm(u64 (&L)[M], int T)
 //   negated (E >= N', or the signs differ):  ~out + 1 + (1 + T_q) 2^E'.
 // After pw_norm T_q = -1, so the (1 + T_q) term is a rare branch, and the whole sum is
 // one add-with-carry chain with carry-in 1.
-template <int M, int LK>
+template <int M, int LK, int PD = 2 * M>
 __host__ __device__ __forceinline__ void pw_combine(u64 (&L)[M], int &T, int &S, int alpha, const u32 *Xw,
                                                    const int *TT, int q, unsigned E)
 {
@@ -110,11 +120,13 @@ __host__ __device__ __forceinline__ void pw_combine(u64 (&L)[M], int &T, int &S,
     // Yw = -1 also reads row 2M at k = 2M - 1 (unused by the funnel): the buffer has it.
     u32 wprev = (-1 < Yw ? bw : bn)[-K] ^ (-1 < Yw ? ~smask : smask);
     u32 c = 1;
-    // every partner word is read before the first is used: all NW LDS reads in flight at once
-    // (one or two at a time, the compiler's default here, exposed the LDS latency per word)
+    // partner words are read PD ahead of their use: all NW at once by default (one or two
+    // at a time, the compiler's own order, exposed the LDS latency per word); a bounded
+    // distance where the kernel must fit 128 VGPRs (pw_wpe: more waves hide the latency)
+    constexpr int D0 = PD < NW ? PD : NW;
     u32 wv[NW];
 #pragma unroll
-    for (int k = 0; k < NW; ++k) {
+    for (int k = 0; k < D0; ++k) {
         const bool wr = k < Yw;
         wv[k] = (wr ? bw : bn)[k * K];
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -123,6 +135,10 @@ __host__ __device__ __forceinline__ void pw_combine(u64 (&L)[M], int &T, int &S,
     }
 #pragma unroll
     for (int k = 0; k < NW; ++k) {
+        if (k + D0 < NW) {
+            const bool wr2 = k + D0 < Yw;
+            wv[k + D0] = (wr2 ? bw : bn)[(k + D0) * K];
+        }
         const bool wr = k < Yw;
         const u32 w = wv[k] ^ (wr ? ~smask : smask);
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -135,6 +151,9 @@ __host__ __device__ __forceinline__ void pw_combine(u64 (&L)[M], int &T, int &S,
         const u32 r = __builtin_addc(lw, o, c, &c);
         if (k & 1) L[k >> 1] = (L[k >> 1] & 0xffffffffull) | ((u64)r << 32);
         else L[k >> 1] = (L[k >> 1] & ~0xffffffffull) | r;
+#if defined(__HIP_DEVICE_COMPILE__)
+        if (D0 < NW && (k & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+#endif
     }
     T += (int)c;
     if (Tq != -1) {   // rare: add cv 2^E', cv = -(1 + T_q) (negated when E >= N')
@@ -262,6 +281,9 @@ __host__ __device__ __forceinline__ void pw_mulmod(u64 (&Z)[M], int &T, const u6
         const int i0 = c < ND ? 0 : c - ND + 1, i1 = c < ND ? c : ND - 1;
 #pragma clang loop unroll(full)
         for (int i = i0; i <= i1; ++i) col += (u64)ad[i] * bd[c - i];
+#if defined(__HIP_DEVICE_COMPILE__)
+        __builtin_amdgcn_sched_barrier(0);   // one column's products live at a time (VGPRs)
+#endif
         acc += (u128)col << (DB * c - pos);
         const bool last = c == 2 * ND - 2;
 #pragma unroll
@@ -345,13 +367,13 @@ __device__ __forceinline__ void pw_transform(u64 (&L)[M], int &T, int &S, unsign
         if (DIR == 0) {
             // top: X_t + X_q = 2^P (x_t + 2^(Pq-P) x_q); bottom: (X_q - X_t) w^tw = 2^(P+tw) (2^(Pq-P) x_q - x_t)
             E = pw_mod(Pq + N2 - P, N2);
-            pw_combine<M, LK>(L, T, S, top ? 1 : -1, Xw, TT, q, E);
+            pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, top ? 1 : -1, Xw, TT, q, E);
             if (!top) P = pw_mod(P + tw, N2);
         } else {
             // top: Z_t + Z_q w^-tw = 2^P (z_t + 2^(Pq-tw-P) z_q)
             // bottom: Z_q - Z_t w^-tw = 2^(P-tw) (2^(Pq-P+tw) z_q - z_t)
             E = top ? pw_mod(Pq + 2 * N2 - tw - P, N2) : pw_mod(Pq + N2 - P + tw, N2);
-            pw_combine<M, LK>(L, T, S, top ? 1 : -1, Xw, TT, q, E);
+            pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, top ? 1 : -1, Xw, TT, q, E);
             if (!top) P = pw_mod(P + N2 - tw, N2);
         }
         if (cross) __syncthreads(); else pw_wave_sync();
@@ -436,7 +458,7 @@ __device__ __forceinline__ void pw_load_pair_bfly(u64 (&L)[M], int &T, const u64
 
 // inner product of one slot: forward transforms of the pieces (La, Ta), (Lb, Tb), the
 // pointwise products in R', the inverse and the un-weighting; leaves the signed
-// coefficients c_t in X (limb-major, M + 1 rows) and their signs in TT (ends with a barrier)
+// coefficients c_t in X (limb-major, M rows) and their signs (+ limb M) in TT (ends with a barrier)
 template <int M, int LK>
 __device__ __forceinline__ void pw_slot_product(u64 (&La)[M], int Ta, u64 (&Lb)[M], int Tb, u64 *X, u32 *Xw, int *TT,
                                                 unsigned *PP, int t, unsigned long long *stamp)
@@ -480,7 +502,7 @@ __device__ __forceinline__ void pw_slot_product(u64 (&La)[M], int Ta, u64 (&Lb)[
         if (half) pw_sqrt2<M>(Z, Tz);
         pw_publish<M, LK>(Z, Tz, Sz, Xw, TT, t);
         pw_wave_sync();                                  // own column only
-        pw_combine<M, LK>(Z, Tz, Sz, 0, Xw, TT, t, F);   // clears the sign flag
+        pw_combine<M, LK, pw_pd<M, LK>()>(Z, Tz, Sz, 0, Xw, TT, t, F);   // clears the sign flag
         __syncthreads();                                 // the u64 rows below cross columns
     }
     // signed coefficient c_t = v - s p', v in [0, 2^N'], s = (v > 2^(N'-1))
@@ -488,8 +510,7 @@ __device__ __forceinline__ void pw_slot_product(u64 (&La)[M], int Ta, u64 (&Lb)[
     const int neg = zt || (Z[M - 1] >> 63);
 #pragma unroll
     for (int j = 0; j < M; ++j) X[j * K + t] = Z[j];
-    X[(size_t)M * K + t] = (u64)zt;              // limb M of v (2^N' only)
-    TT[t] = neg;
+    TT[t] = neg | (zt << 1);                     // s, and limb M of v (2^N' only)
     __syncthreads();
     PW_STAMP(6);
 #undef PW_STAMP
@@ -498,7 +519,7 @@ __device__ __forceinline__ void pw_slot_product(u64 (&La)[M], int Ta, u64 (&Lb)[
 // R = sum_t c_t 2^(B t) mod 2^N + 1 from X / TT, stored in the reduced HBM form at
 // (pa, cbp, *topp).  c_t 2^(Bt) = v_t 2^(Bt) - s_t (2^(Bt) + 2^(N' + Bt)); positions >= N
 // wrap negated.  Thread t of NTH sums output limbs m = t + NTH r (coalesced, consecutive
-// per wave).
+// per wave).  H (the l limb overflows) aliases X: written after a barrier.
 template <int M, int LK, int NTH = (1 << LK)>
 __device__ __forceinline__ void pw_slot_output(const u64 *X, const int *TT, int *H, u64 *pa, u64 *cbp, int *topp, int l,
                                                int t)
@@ -526,15 +547,19 @@ __device__ __forceinline__ void pw_slot_output(const u64 *X, const int *TT, int 
             if (hi > K - 1) hi = K - 1;
             for (int tp = lo; tp <= hi; ++tp) {
                 const int d = mm - tp * LP;        // limb of c_tp, 0 .. M
-                i128 v = (i128)X[(size_t)d * K + tp];
-                if (TT[tp] && (d == 0 || d == M)) v -= 1;
+                const int tt = TT[tp];
+                i128 v = d < M ? (i128)X[(size_t)d * K + tp] : (i128)(tt >> 1);
+                if ((tt & 1) && (d == 0 || d == M)) v -= 1;
                 S += wrap ? -v : v;
             }
         }
         fo[r] = (u64)S;
         ho[r] = (int)(i64)(S >> 64);
-        H[m] = ho[r];
     }
+    __syncthreads();   // every X read done: H overwrites its first rows
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+        if (r < RPT) H[t + NTH * r] = ho[r];
     __syncthreads();
     // limb m: f_m + hv_(m-1) -> limb + carry out in {-1, 0, 1} (reduced form; the top
     // limb's overflow wraps into limb 0 negated, and its carry weighs 2^N == -1)
@@ -567,7 +592,7 @@ __device__ __forceinline__ void pw_slot_output(const u64 *X, const int *TT, int 
 // (Fusing the inverse row DIT's first level as well needs both products in one workgroup:
 // measured at 194-256 VGPRs, occupancy 2 -> 1, so the inverse side stays a pass.)
 template <int M, int LK, int FUSE>
-__global__ __launch_bounds__(1 << LK) void k_pwss(u64 *digA, u64 *cbA, int *topA, const u64 *digB, const u64 *cbB,
+__global__ __launch_bounds__(1 << LK) __attribute__((amdgpu_waves_per_eu(pw_wpe<M, LK>()))) void k_pwss(u64 *digA, u64 *cbA, int *topA, const u64 *digB, const u64 *cbB,
                                                   const int *topB, int l, u64 *digC, u64 *cbC, int *topC,
                                                   unsigned long long *dbg)
 {
@@ -577,11 +602,11 @@ __global__ __launch_bounds__(1 << LK) void k_pwss(u64 *digA, u64 *cbA, int *topA
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int K = 1 << LK;
     const int t = threadIdx.x;
-    u64 *X = (u64 *)smem;                        // (M + 1) K limbs (words 2M + 2 rows during the transforms)
+    u64 *X = (u64 *)smem;                        // M K limbs (2M word rows during the transforms)
     u32 *Xw = (u32 *)smem;
-    int *TT = (int *)(X + (size_t)(M + 1) * K);  // K
+    int *TT = (int *)(X + (size_t)M * K);        // K
     unsigned *PP = (unsigned *)(TT + K);         // K
-    int *H = (int *)(PP + K);                    // l
+    int *H = (int *)smem;                        // l, over X (pw_slot_output)
     const int cbw = cb_words(l);
     constexpr int CLP = pw_piece_limbs<M, LK>();   // == l / K (host: pw_inner_limbs)
     u64 La[M], Lb[M];
