@@ -1,0 +1,70 @@
+"""GPU check of the (depth, w) chooser (mpfft_choose): at four operand
+sizes the chosen configuration is timed against every other valid candidate whose
+coefficient size is within 4x of the chosen one, and must be within 15 % of the fastest
+(device-resident operands, the mpfft_mul_device path).  The reference leaves (depth, w)
+to its caller (mul_fft.c:3190-3191); the chooser's cost table comes from
+scripts/chooser_sweep.py (profiles/r02/chooser_sweep.json)."""
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def _candidates(mp, n1, n2):
+    out = []
+    for d in range(2, 25):
+        wv = 1
+        while wv <= 4096:
+            N = (1 << d) * wv
+            if N % 64 == 0 and N // 64 <= 4096 and mp.check_params(n1, n2, d, wv) == 0:
+                out.append((d, wv))
+            wv *= 2
+    return out
+
+
+def _time(mp, torch, dev, a, b, n1, n2, d, wv, reps):
+    r = torch.zeros(n1 + n2, dtype=torch.int64, device=dev)
+    ws = mp.alloc_workspace(n1, n2, d, wv, dev)
+    mp.mul_device(r, a, n1, b, n2, d, wv, ws)          # warm-up (code objects, caches)
+    torch.cuda.synchronize()
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        mp.mul_device(r, a, n1, b, n2, d, wv, ws)
+        torch.cuda.synchronize()
+        t = time.perf_counter() - t0
+        best = t if best is None else min(best, t)
+    del r, ws
+    return best
+
+
+@pytest.mark.parametrize("n", [100000, 1000000, 4000000, 15625000])
+def test_chooser_within_15_percent_of_best(mp, torch_dev, n):
+    import torch
+    n1, n2 = n, n
+    d0, w0 = mp.choose(n1, n2)
+    l0 = mp.plan_info(n1, n2, d0, w0)["l"]
+    cands = [(d, wv) for d, wv in _candidates(mp, n1, n2)
+             if l0 // 4 <= mp.plan_info(n1, n2, d, wv)["l"] <= 4 * l0]
+    assert (d0, w0) in cands
+    a = torch.from_numpy(mp.fill_random(n1, 5).view(np.int64)).to(torch_dev)
+    b = torch.from_numpy(mp.fill_random(n2, 6).view(np.int64)).to(torch_dev)
+    reps = 5 if n <= 1000000 else 3
+    times = {c: _time(mp, torch, torch_dev, a, b, n1, n2, c[0], c[1], reps) for c in cands}
+    torch.cuda.empty_cache()
+    best = min(times.values())
+    ranked = sorted(times.items(), key=lambda kv: kv[1])
+    msg = ", ".join(f"(d={d}, w={wv}, l={mp.plan_info(n1, n2, d, wv)['l']}): {t * 1e3:.3f} ms"
+                    for (d, wv), t in ranked[:6])
+    print(f"n={n}: chosen (d={d0}, w={w0}, l={l0}) {times[(d0, w0)] * 1e3:.3f} ms; best {msg}")
+    assert times[(d0, w0)] <= 1.15 * best, msg
