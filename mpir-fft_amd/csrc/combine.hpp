@@ -20,6 +20,7 @@ struct CombArgs {
     int NC, cbb, ccb;    // row layout: k -> p = k / NC - r0, c = k % NC,
     long cbs;            //   slot = (c >> cbb) * cbs + p * ccb + (c & (ccb - 1))
     long r0;
+    double inv_bits1;    // 1.0 / bits1 (host), for the window bounds
 };
 
 // --------------------------------------------------------------------------
@@ -56,33 +57,51 @@ __device__ __forceinline__ const u64 *coef_ptr2(const CombArgs &a, long k)
     return a.dig + (size_t)slot * a.l;
 }
 
+// floor(x / d) for x < 2^52 from a precomputed inv = fl(1/d): the double product is within
+// 1 of x / d, one fix-up each way
+__device__ __forceinline__ long udiv_inv(u64 x, u64 d, double inv)
+{
+    long q = (long)((double)x * inv);
+    if ((u64)q * d > x) --q;
+    else if ((u64)(q + 1) * d <= x) ++q;
+    return q;
+}
+
 // m: global product limb (a.m0 + local index); coefficients below kbase come from the halo
-// (a rank's combine in the sharded multiply), the rest from the row layout
+// (a rank's combine in the sharded multiply), the rest from the row layout.
+// KM > 0: at most KM coefficients cover a limb (host: ceil((N + 63) / bits1) <= KM), a
+// fixed-trip loop of guarded loads, so a thread's loads for all its limbs can be in flight
+// together (the combine is latency-bound otherwise); KM = 0: any count.
+template <int KM>
 __device__ __forceinline__ void comb_limb(const CombArgs &a, long m, u64 *lo, u32 *hi)
 {
     const u64 P = (u64)m * 64;
-    long klo = (P >= a.N) ? udiv_exact(P - a.N, a.bits1) : 0;
-    long khi = udiv_exact(P + 63, a.bits1);
+    // first coefficient reaching past bit P (k bits1 + N > P) .. last starting below P + 64
+    const long klo = (P >= a.N) ? udiv_inv(P - a.N, a.bits1, a.inv_bits1) + 1 : 0;
+    long khi = udiv_inv(P + 63, a.bits1, a.inv_bits1);
     if (khi > a.len - 1) khi = a.len - 1;
     u64 slo = 0;
     u32 shi = 0;
-    for (long k = klo; k <= khi; ++k) {
+    auto window = [&](long k, bool in) {
+        // c_k at bit P: o = P - st + 64 in [1, N + 63]; words q = o / 64 - 1 and q + 1 (word -1,
+        // before the coefficient, and words >= l read as 0)
         const u64 st = (u64)k * a.bits1;
+        const u64 o = P + 64 - st;
+        const long q = (long)(o >> 6) - 1;
+        const int sb = (int)(o & 63);
         const u64 *cp = k < a.kbase ? a.halo + (size_t)(k - (a.kbase - a.H)) * a.l : coef_ptr2(a, k);
-        u64 v;
-        if (st > P) {
-            v = cp[0] << (st - P);
-        } else {
-            const u64 o = P - st;
-            const long q = (long)(o >> 6);
-            const int s = (int)(o & 63);
-            const u64 w0 = (q < a.l) ? cp[q] : 0;
-            const u64 w1 = (s && q + 1 < a.l) ? cp[q + 1] : 0;
-            v = s ? (w0 >> s) | (w1 << (64 - s)) : w0;
-        }
+        const u64 w0 = (in && q >= 0 && q < a.l) ? cp[q] : 0;
+        const u64 w1 = (in && sb && q + 1 < a.l) ? cp[q + 1] : 0;
+        const u64 v = sb ? (w0 >> sb) | (w1 << (64 - sb)) : w0;
         u64 t;
         shi += add_ovf(slo, v, &t);
         slo = t;
+    };
+    if constexpr (KM > 0) {
+#pragma unroll
+        for (int j = 0; j < KM; ++j) window(klo + j, klo + j <= khi);
+    } else {
+        for (long k = klo; k <= khi; ++k) window(k, true);
     }
     *lo = slo;
     *hi = shi;
@@ -92,7 +111,7 @@ __device__ __forceinline__ void comb_limb(const CombArgs &a, long m, u64 *lo, u3
 // starts from carry-in 0 and the overflow of limb m0 - 1; its carry-out with that carry-in
 // ends in st[nblocks - 1] (4 + carry) and, when `allp` is given, allp[b] = 1 for every block
 // whose limbs all propagate (k_comb_summary turns both into the rank's (generate, propagate)).
-template <int CB_V>
+template <int CB_V, int KM>
 __global__ __launch_bounds__(256) void k_combine1(CombArgs a, u64 *r, u32 *st, u32 *allp_out)
 {
     constexpr int CB_LIMBS = 256 * CB_V;
@@ -113,14 +132,14 @@ __global__ __launch_bounds__(256) void k_combine1(CombArgs a, u64 *r, u32 *st, u
         const long m = base + i;
         u64 lo = 0;
         u32 hi = 0;
-        if (m < total) comb_limb(a, a.m0 + m, &lo, &hi);
+        if (m < total) comb_limb<KM>(a, a.m0 + m, &lo, &hi);
         L[i] = lo;
         H[i + 1] = hi;
     }
     if (c.t == 0) {
         u64 lo = 0;
         u32 hi = 0;
-        if (a.m0 + base > 0) comb_limb(a, a.m0 + base - 1, &lo, &hi);
+        if (a.m0 + base > 0) comb_limb<KM>(a, a.m0 + base - 1, &lo, &hi);
         H[0] = hi;
     }
     __syncthreads();

@@ -947,11 +947,16 @@ struct Exec {
         a.ccb = ccb;
         a.cbs = cbs;
         a.r0 = r0;
+        a.inv_bits1 = 1.0 / (double)P.bits1;
         const long nb = comb_blocks(mcount);
         if (!cleared) HIPCHK(hipMemsetAsync(st, 0, (size_t)comb_flag_words(mcount) * 4, s));   // one fill
         const int v = comb_v();
-        void (*f)(CombArgs, u64 *, u32 *, u32 *) = v == 1 ? k_combine1<1> : v == 2 ? k_combine1<2>
-                                                 : v == 4 ? k_combine1<4> : v == 16 ? k_combine1<16> : k_combine1<8>;
+        const bool k3 = (P.N + 63 + P.bits1 - 1) / P.bits1 <= 3;   // at most 3 coefficients cover a limb
+        void (*f)(CombArgs, u64 *, u32 *, u32 *) =
+            k3 ? (v == 1 ? k_combine1<1, 3> : v == 2 ? k_combine1<2, 3> : v == 4 ? k_combine1<4, 3>
+                  : v == 16 ? k_combine1<16, 3> : k_combine1<8, 3>)
+               : (v == 1 ? k_combine1<1, 0> : v == 2 ? k_combine1<2, 0> : v == 4 ? k_combine1<4, 0>
+                  : v == 16 ? k_combine1<16, 0> : k_combine1<8, 0>);
         hipLaunchKernelGGL(f, dim3((unsigned)nb), dim3(256), 0, s, a, r, st, allp);   // st[nb]: the ticket counter
         HIPCHK(hipGetLastError());
         return MPFFT_OK;
