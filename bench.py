@@ -29,6 +29,7 @@ Fields beyond the driver contract:
 import argparse
 import hashlib
 import json
+import statistics
 import os
 import socket
 import subprocess
@@ -93,25 +94,36 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(a, b, depth, w, budget_s):
-    """oracle/ new_mpn_mul (1 thread) on the bench operands; GMP mpn_mul beside it."""
+def cpu_baseline(a, b, depth, w, reps, warmup=1):
+    """oracle/ new_mpn_mul (1 thread) on the bench operands, pinned to one core (BASELINE.md's
+    `taskset -c 0` protocol): `warmup` untimed calls, then the median of `reps` timed calls;
+    GMP mpn_mul on the same operands beside it."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    reps, t0 = 0, time.perf_counter()
-    ref = None
-    while True:
-        ref = O.new_mpn_mul(a, b, depth, w)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or reps >= 1000:
-            break
-    t1 = time.perf_counter()
-    g = O.gmp_mul(a, b)
-    tg = time.perf_counter() - t1
+    old = os.sched_getaffinity(0)
+    core = min(old)
+    os.sched_setaffinity(0, {core})
+    try:
+        ref = None
+        for _ in range(warmup):
+            ref = O.new_mpn_mul(a, b, depth, w)
+        times = []
+        for _ in range(max(1, reps)):
+            t0 = time.perf_counter()
+            ref = O.new_mpn_mul(a, b, depth, w)
+            times.append(time.perf_counter() - t0)
+        t1 = time.perf_counter()
+        g = O.gmp_mul(a, b)
+        tg = time.perf_counter() - t1
+    finally:
+        os.sched_setaffinity(0, old)
+    med = statistics.median(times)
     n = len(a) + len(b)
-    return {"value": n * reps / el, "unit": "limbs/s", "cores": 1, "kind": "port",
-            "sample": f"{reps} full new_mpn_mul of the bench operands via oracle/ (CPU restatement of "
-                      f"mul_fft.c:3190, single thread), {el:.1f} s",
+    return {"value": n / med, "unit": "limbs/s", "cores": 1, "kind": "port",
+            "sample": f"median of {len(times)} full new_mpn_mul calls of the bench operands via oracle/ "
+                      f"(CPU restatement of mul_fft.c:3190, single thread pinned to core {core}) after "
+                      f"{warmup} warm-up: {med:.2f} s per call (min {min(times):.2f}, max {max(times):.2f})",
+            "seconds_per_call": times,
             "gmp_mpn_mul_limbs_per_s": n / tg, "gmp_mpn_mul_s": tg,
             "cpu_model": cpu_model(), "nproc": os.cpu_count()}, ref, g
 
@@ -192,7 +204,8 @@ def main():
                     help="default: C3 at N = 1, C4 at N > 1 (M4: --mul6 only)")
     ap.add_argument("--mode", default=None, choices=["single", "replicas", "sharded"],
                     help="N > 1: sharded (default) or independent replicas")
-    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of oracle sampling (>= 1 call)")
+    ap.add_argument("--cpu-reps", type=int, default=5, help="timed oracle calls (median; after one warm-up)")
+    ap.add_argument("--cpu-warmup", type=int, default=1, help="untimed oracle calls before the timed ones")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--e2e-reps", type=int, default=2)
@@ -367,7 +380,7 @@ def main():
         "exact_check": "SHA-256 of the product limbs vs tests/golden/products.json (GMP mpn_mul)",
     }
     if world == 1 and not args.no_cpu_baseline:
-        cb, ref, g = cpu_baseline(a, b, depth, w, args.cpu_budget)
+        cb, ref, g = cpu_baseline(a, b, depth, w, args.cpu_reps, args.cpu_warmup)
         res["cpu_baseline"] = cb
         res["exact_vs_port"] = bool((got == ref).all())
         res["exact_vs_gmp"] = bool((got == g).all())
