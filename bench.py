@@ -339,7 +339,32 @@ def main():
         te = (time.perf_counter() - t1) / args.e2e_reps
         e2e = {"ms": te * 1e3, "limbs_per_s": (n1 + n2) / te, "same_product": bool((r == got).all()),
                "note": "host arrays: H2D of both operands, the multiply, D2H of the product (PCIe included)"}
-        del r
+        # the host link on its own (same pageable arrays; a pinned copy beside it): operand 1's H2D
+        # cannot overlap the multiply (its first column pass reads the whole operand) and the
+        # product's D2H cannot start before the combine, so h2d(i1) + device + d2h(r) bounds e2e
+        ta, tr = torch.from_numpy(a), torch.from_numpy(r)
+        dbuf = torch.empty(n1 + n2, dtype=torch.int64, device=dev)
+
+        def rate(fn, nbytes, reps=3):
+            fn()
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            torch.cuda.synchronize()
+            return nbytes * reps / (time.perf_counter() - t) / 1e9
+
+        h2d = rate(lambda: dbuf[:n1].copy_(ta.view(torch.int64)), n1 * 8)
+        d2h = rate(lambda: tr.view(torch.int64).copy_(dbuf), (n1 + n2) * 8)
+        pa, pr = ta.view(torch.int64).pin_memory(), tr.view(torch.int64).pin_memory()
+        h2d_p = rate(lambda: dbuf[:n1].copy_(pa, non_blocking=True), n1 * 8)
+        d2h_p = rate(lambda: pr.copy_(dbuf, non_blocking=True), (n1 + n2) * 8)
+        e2e["link"] = {"h2d_pageable_GBs": h2d, "d2h_pageable_GBs": d2h, "h2d_pinned_GBs": h2d_p,
+                       "d2h_pinned_GBs": d2h_p,
+                       "bound_ms": (n1 * 8 / h2d + (n1 + n2) * 8 / d2h) * 1e-6 + el / args.steps * 1e3,
+                       "note": "bound = H2D of operand 1 + device multiply + D2H of the product at the "
+                               "pageable rates measured here (operand 2's H2D overlaps operand 1's transform)"}
+        del r, ta, tr, dbuf, pa, pr
         mp.lib().mpfft_release()
 
     if rank != 0:

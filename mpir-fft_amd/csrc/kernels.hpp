@@ -53,6 +53,11 @@ struct PassArgs {
     unsigned *zp;        // non-null: clear zp[0, zn) (the combine's look-back flags) -- saves a fill launch
     long zn;
     unsigned long long *dbg;   // diagnostics only (MPFFT_BP_STAMPS): per-workgroup s_memtime phase stamps
+    // Pending exponents carried across k_rpass DIF passes (rkernels.hpp, single-GPU run_all only):
+    int pcarry;          // the inputs still owe the DIF pending exponents of levels [lvl0 - pcarry, lvl0)
+    int pkeep;           // leave every pending exponent in the output (the next pass applies them)
+    int ccarry;          // first row pass (tw_mode 1): the input owes the column DIF's pending
+                         // exponents of levels [tw_lbR - ccarry, tw_lbR) at its row
 };
 
 // Grid-stride clear of PassArgs::zp; called at the top of every pass kernel, before

@@ -205,7 +205,9 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
         const char *er = diag_env("MPFFT_RPASS");
         p->rpass = rp_maxlogg((int)p->l) > 0 && !(er && !strcmp(er, "0")) && !diag_env("MPFFT_BP_STAMPS");
         if (p->rpass && !e) {   // same levels per pass for columns and rows (two groups per CU either way)
-            const int rl = rp_maxlogg((int)p->l) < lg ? rp_maxlogg((int)p->l) : lg;
+            int rl = rp_maxlogg((int)p->l);   // register-resident: not bound by k_bpass's LDS fit
+            const char *ec = diag_env("MPFFT_RPLOGG");   // diagnostics: fewer levels per pass (A/B)
+            if (ec && atoi(ec) >= 1 && atoi(ec) < rl) rl = atoi(ec);
             p->maxlogg = p->maxlogg_c = rl;
         }
     }
@@ -309,6 +311,19 @@ struct Exec {
     int in_rows = 0;         // non-zero: inputs live in column rows [0, in_rows) (default: the trunc rows)
     bool defer_double = false;   // itft's top-level doubling is left to scale() (rows [dbl_lo, dbl_hi): 2^-depth)
     bool fuse_row_last = false;  // the row DIF's last level runs inside the pointwise (k_pwss PAIR)
+    bool carry_pend = false;     // forward k_rpass passes hand their pending exponents on (fwd_columns)
+    // which hand-overs: 1 column -> column, 2 last column -> first row (its MFA twiddle rotation
+    // absorbs them; a no-op in practice: after a transform's last level every DIF pending
+    // exponent is 0), 4 row -> row.  A hand-over into a plain pass moves that pass's first level
+    // from registers to an LDS round, about what the skipped closing round costs: measured
+    // (profiles/r03/carry_ab.txt) row -> row pays at l = 2048 and 4096, column -> column only
+    // at l = 4096 (C3 columns 2.02 -> 2.08 ms with it, C4 20.7 -> 19.9 ms).
+    int carry_mask() const
+    {
+        static const int m = [] { const char *e = diag_env("MPFFT_CARRY_MASK"); return e ? atoi(e) : -1; }();
+        return m >= 0 ? m : P.l >= 4096 ? 7 : 6;
+    }
+    int col_carry = 0;           // column levels whose pending exponents the first row pass applies
     long dbl_lo = 0, dbl_hi = 0;
 
     Exec(const Plan &p, hipStream_t st) : P(p), s(st) { nw = P.tpb / 64; }
@@ -390,19 +405,27 @@ struct Exec {
         if (!P.rpass || logg > rp_maxlogg((int)P.l) || a.canon || a.rho % 128) return -1;
         if (dir == 0) {
             if (a.scale_e || a.tw_mode == 2) return -1;
-            if (a.src[0] || a.src[1]) return a.tw_mode ? -1 : 2;
+            if (a.src[0] || a.src[1]) return a.tw_mode || a.pcarry ? -1 : 2;
             if (a.zero_from < (1 << a.lbM)) return -1;
-            return a.tw_mode == 1 ? 1 : 0;
+            if (a.tw_mode == 1) return a.pcarry ? -1 : 1;
+            return a.pcarry ? 3 : 0;
         }
         if (a.tw_mode == 1) return -1;
-        return (a.tw_mode == 2 || a.scale_e) ? 1 : 0;
+        return ((a.tw_mode == 2 || a.scale_e) ? 1 : 0) | (a.lvl0 + logg == a.lbM ? 2 : 0);
+    }
+
+    // the k_rpass mode pass() launches for these arguments, -1: another kernel family
+    int rp_mode(const PassArgs &a, int logg, int dir) const
+    {
+        int rm = rpass_mode(a, logg, dir);
+        static const int rmask = [] { const char *e = diag_env("MPFFT_RPASS_OFF"); return e ? atoi(e) : 0; }();
+        if (rm >= 0 && (rmask >> (4 * dir + rm) & 1)) rm = -1;   // diagnostics: bit 4 dir + mode off
+        return rm;
     }
 
     int pass(PassArgs a, int logg, int dir, int nops)
     {
-        int rm = rpass_mode(a, logg, dir);
-        static const int rmask = [] { const char *e = diag_env("MPFFT_RPASS_OFF"); return e ? atoi(e) : 0; }();
-        if (rm >= 0 && (rmask >> (3 * dir + rm) & 1)) rm = -1;   // diagnostics: bit 3 dir + mode off
+        const int rm = rp_mode(a, logg, dir);
         if (rm >= 0) {
             rp_fn f = rp_get((int)P.l, logg, dir, rm);
             if (!f) return MPFFT_EUNSUPPORTED;
@@ -414,8 +437,9 @@ struct Exec {
             a.ngroups = 1 << (a.lbM - logg);
             dim3 grid((unsigned)((long)a.nsub * a.ngroups), (unsigned)nops);
             static const bool stamps = diag_env("MPFFT_RP_STAMPS") != nullptr;
-            if (stamps) return bp_stamped(f, grid, RP_NT, lds, a, logg, dir);
-            hipLaunchKernelGGL(f, grid, dim3(RP_NT), lds, s, a);
+            const unsigned nt = (unsigned)rp_nt((int)P.l, logg);
+            if (stamps) return bp_stamped(f, grid, nt, lds, a, logg, dir);
+            hipLaunchKernelGGL(f, grid, dim3(nt), lds, s, a);
             HIPCHK(hipGetLastError());
             return MPFFT_OK;
         }
@@ -503,7 +527,7 @@ struct Exec {
             for (int k = 1; k < 8; ++k)
                 if (q[k]) { sum[k] += (double)(q[k] - prev); prev = q[k]; }
         }
-        fprintf(stderr, "%s logg=%d dir=%d l=%ld groups=%ld/%zu span=%llu ticks: load %.0f lv0 %.0f lv1 %.0f lv2 %.0f fin %.0f canon/hx %.0f store %.0f\n", nthr == RP_NT ? "rp_stamps" : "bp_stamps",
+        fprintf(stderr, "%s logg=%d dir=%d l=%ld groups=%ld/%zu span=%llu ticks: load %.0f lv0 %.0f lv1 %.0f lv2 %.0f fin %.0f canon/hx %.0f store %.0f\n", nthr == RP_NT || nthr == 1024 ? "rp_stamps" : "bp_stamps",
                 logg, dir, P.l, cnt, nwg, t1 - t0, sum[1] / cnt, sum[2] / cnt, sum[3] / cnt, sum[4] / cnt, sum[5] / cnt,
                 sum[6] / cnt, sum[7] / cnt);
         free(h);
@@ -573,12 +597,30 @@ struct Exec {
         return a;
     }
 
+    // Pending exponents across forward passes (carry_pend, single-GPU run_all / run_all6): a
+    // k_rpass DIF pass whose successor is also a k_rpass DIF pass skips its closing rotation
+    // round (the last level's pending exponents, one LDS round trip of all G coefficients) and
+    // leaves them in HBM; the successor folds them into its first level's partner rotations
+    // (PassArgs::pcarry) or, for the first row pass, into its MFA twiddle (ccarry).  The stage
+    // API and the sharded path keep every pass self-contained (their stage outputs are exact).
+    PassArgs col_pass_args(int lvl) const
+    {
+        PassArgs a = col_args();
+        a.zero_from = (int)P.NR;
+        a.lbM = P.lbR;
+        a.lvl0 = lvl;
+        a.rho = (u64)P.w * P.NC;
+        a.need = (int)P.Tr;
+        return a;
+    }
+
     int fwd_columns(const u64 *srcA, long nA, const u64 *srcB, long nB, int nops, int op = -1)
     {
-        int lvl = 0;
+        int lvl = 0, pend0 = 0;   // the data still owe the pending exponents of levels [pend0, lvl)
+        col_carry = 0;
         while (lvl < P.lbR) {
             int k = split(P.lbR - lvl, true);
-            PassArgs a = col_args();
+            PassArgs a = col_pass_args(lvl);
             if (lvl == 0) {
                 a.src[0] = srcA; a.nsrc[0] = nA;
                 a.src[1] = srcB; a.nsrc[1] = nB;
@@ -586,18 +628,24 @@ struct Exec {
                 a.zero_from = in_rows ? in_rows : (int)P.Tr;
                 a.zp = zflags;
                 a.zn = zflags_n;
-            } else {
-                a.zero_from = (int)P.NR;
             }
-            a.lbM = P.lbR;
-            a.lvl0 = lvl;
-            a.rho = (u64)P.w * P.NC;
-            a.need = (int)P.Tr;
             if (op == 1) a.zp = nullptr;   // the combine flags are cleared by operand 0's pass
+            a.pcarry = lvl - pend0;
+            if (carry_pend && rp_mode(a, k, 0) >= 0 && (carry_mask() & (lvl + k < P.lbR ? 1 : 2))) {
+                if (lvl + k < P.lbR) {
+                    const int k2 = split(P.lbR - lvl - k, true);
+                    a.pkeep = rp_mode(col_pass_args(lvl + k), k2, 0) >= 0;
+                } else {
+                    const int L = row_levels();
+                    a.pkeep = L > 0 && rp_mode(row_pass_args(0, split(L), L), split(L), 0) >= 0;
+                }
+            }
             int rc = op < 0 ? pass(a, k, 0, nops) : pass(only(a, op), k, 0, 1);
             if (rc) return rc;
             lvl += k;
+            if (!a.pkeep) pend0 = lvl;
         }
+        col_carry = P.lbR - pend0;   // consumed by the next fwd_rows
         return MPFFT_OK;
     }
 
@@ -610,22 +658,38 @@ struct Exec {
         return fuse_row_last && !off && P.has_c && cview.dig[0] && pw_pair_kernel(P.l) && ccb >= 2;
     }
 
+    int row_levels() const { return P.lbC - (row_fused() ? 1 : 0); }
+
+    PassArgs row_pass_args(int lvl, int k, int L) const
+    {
+        PassArgs a = row_args();
+        a.lvl0 = lvl;
+        a.tw_mode = lvl == 0 ? 1 : 0;
+        // canonical pointwise inputs, except for k_pwss (it loads the reduced form)
+        if (lvl + k == L) a.canon = pwss_active() ? 0 : 1;
+        return a;
+    }
+
     // stage 2: MFA twiddle + row DIF (length NC, root 2^(w NR)), canonical out
     int fwd_rows(int nops, int op = -1)
     {
-        int lvl = 0;
-        const int L = P.lbC - (row_fused() ? 1 : 0);
+        int lvl = 0, pend0 = 0;
+        const int L = row_levels();
         while (lvl < L) {
             int k = split(L - lvl);
-            PassArgs a = row_args();
-            a.lvl0 = lvl;
-            a.tw_mode = lvl == 0 ? 1 : 0;
-            // canonical pointwise inputs, except for k_pwss (it loads the reduced form)
-            if (lvl + k == L) a.canon = pwss_active() ? 0 : 1;
+            PassArgs a = row_pass_args(lvl, k, L);
+            a.pcarry = lvl - pend0;
+            if (lvl == 0) a.ccarry = col_carry;
+            if (carry_pend && (carry_mask() & 4) && lvl + k < L && rp_mode(a, k, 0) >= 0) {
+                const int k2 = split(L - lvl - k);
+                a.pkeep = rp_mode(row_pass_args(lvl + k, k2, L), k2, 0) >= 0;
+            }
             int rc = op < 0 ? pass(a, k, 0, nops) : pass(only(a, op), k, 0, 1);
             if (rc) return rc;
             lvl += k;
+            if (!a.pkeep) pend0 = lvl;
         }
+        col_carry = 0;
         return MPFFT_OK;
     }
 
@@ -1063,35 +1127,44 @@ static int run_all6(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, u
     X2.shift(2 * P.n);
     X2.in_rows = (int)P.NR;   // the second half's inputs are all live (FFT_radix2_truncate1_twiddle)
     X1.fuse_row_last = X2.fuse_row_last = true;   // each half's last row level inside its pointwise
+    X1.carry_pend = X2.carry_pend = !diag_env("MPFFT_NO_CARRY");
     XS.single(ws);
     XC.single(ws);
     const bool two = P2.Tr > 0;
     const long tlo = P.trunc - 2 * P.n;   // pairs k < tlo carry both halves
     int rc;
+    ProfCall pc;   // stage events as run_all's (the sqrt2 top level counts with the columns)
+    pc.mark(0, s);
     if ((rc = s2_launch(P, X1, S2_FWD, d_i1, d_i2, 0, 2 * P.n, two ? 1 : 0, 2))) return rc;
     if ((rc = X1.fwd_columns(nullptr, 0, nullptr, 0, 2))) return rc;
+    if (two && (rc = X2.fwd_columns(nullptr, 0, nullptr, 0, 2))) return rc;
+    pc.mark(1, s);
     if ((rc = X1.fwd_rows(2))) return rc;
-    if (two) {
-        if ((rc = X2.fwd_columns(nullptr, 0, nullptr, 0, 2))) return rc;
-        if ((rc = X2.fwd_rows(2))) return rc;
-    }
+    if (two && (rc = X2.fwd_rows(2))) return rc;
+    pc.mark(2, s);
     const bool fused = X1.row_fused();
     if ((rc = X1.pointwise())) return rc;
     if (two && (rc = X2.pointwise())) return rc;
+    pc.mark(3, s);
     if (fused) {   // the products (and everything after) live in C: X1's views now start there
         XS.col = XS.row = X1.col;
         XC.col = XC.row = X1.col;
     }
     if ((rc = X1.inv_rows())) return rc;
     if (two && (rc = X2.inv_rows())) return rc;
+    pc.mark(4, s);
     if ((rc = X1.itft(0, P.NR, P.NR))) return rc;
     if (two) {
         if ((rc = s2_launch(P, X1, S2_FILL, nullptr, nullptr, P2.Tr * P.NC, (P.NR - P2.Tr) * P.NC, 0, 1))) return rc;
         if ((rc = X2.itft1(0, P.NR, P2.Tr))) return rc;
     }
     if ((rc = s2_launch(P, X1, S2_IBFLY, nullptr, nullptr, 0, 2 * P.n, tlo > 0 ? tlo : 0, 1))) return rc;
+    pc.mark(5, s);
     if ((rc = XS.scale())) return rc;
-    return XC.combine_single(d_r, ws);
+    pc.mark(6, s);
+    rc = XC.combine_single(d_r, ws);
+    pc.mark(7, s);
+    return rc;
 }
 
 // Host operands (mul_host): operand 2's copy from the host runs on the context's copy stream
@@ -1112,6 +1185,7 @@ static int run_all(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, un
     X.zflags_n = X.comb_flag_words(P.total);
     X.defer_double = true;   // itft + scale back to back
     X.fuse_row_last = true;  // last row level inside the pointwise (nested negacyclic sizes)
+    X.carry_pend = !diag_env("MPFFT_NO_CARRY");
     ProfCall pc;
     int rc;
     pc.mark(0, s);

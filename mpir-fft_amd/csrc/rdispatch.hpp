@@ -11,16 +11,25 @@ typedef void (*rp_pair_fn)(PairArgs);
 
 #define RP_NT 512   // threads per workgroup; two workgroups share a CU
 
+// k_rpass at l = 4096 with three levels (G = 8: 256 KiB of coefficients per group) runs
+// 1024 threads, one workgroup per CU: every thread still holds 16 limb pairs (80 VGPRs)
+constexpr int rp_nt(int l, int logg) { return l == 4096 && logg == 3 ? 1024 : RP_NT; }
+// limb pairs per thread and coefficient (thread t owns pairs t + NT r)
+constexpr int rp_r(int PP, int NT) { return 512 * PP / NT; }
+
 // k_rpass<LOGG, PP, DIR, MODE> for coefficients of l = 1024 PP limbs (PP = 1, 2, 4);
-// MODE: DIR 0: 1 = MFA twiddle applied on load, 2 = split fused into the load;
-//       DIR 1: 1 = general final multipliers (inverse twiddle, scaling).
+// MODE: DIR 0: 1 = MFA twiddle applied on load, 2 = split fused into the load, 3 = inputs
+//               owe an earlier pass's pending exponents (PassArgs::pcarry);
+//       DIR 1: bit 0 = general final multipliers (inverse twiddle, scaling), bit 1 = the
+//               pass holds the transform's last level.
 rp_fn rp_get(int l, int logg, int dir, int mode);
 
-// most levels per pass: G l <= 16384 limbs per workgroup (32 limbs per thread)
-inline int rp_maxlogg(int l) { return l == 1024 ? 3 : l == 2048 ? 3 : l == 4096 ? 2 : 0; }   // l = 1024: G = 16 spills
+// most levels per pass: 32 limbs per thread (G l <= 16384 limbs per 512-thread workgroup,
+// 32768 at l = 4096 with 1024 threads)
+inline int rp_maxlogg(int l) { return l == 1024 ? 3 : l == 2048 ? 3 : l == 4096 ? 3 : 0; }   // l = 1024: G = 16 spills
 
 // LDS: NX exchange slots of 9 l bytes (limbs + 16-bit pair overflows) and the exponent
-// table.  <= 73 984 B, so two workgroups fit in 160 KiB.
+// table.  <= 73 984 B, so two workgroups fit in 160 KiB (l = 4096, G = 8: 147 600 B, one).
 inline size_t rp_lds(int l, int logg)
 {
     const int G = 1 << logg, NX = G / 2 > 2 ? G / 2 : 2;

@@ -127,12 +127,12 @@ struct RX {
     __device__ __forceinline__ short *h(int j) const { return (short *)(base + (size_t)j * SB + 8 * (size_t)l); }
 };
 
-template <int PP>
-__device__ __forceinline__ void rp_pub(const RX<PP> &X, int j, const Pr (&x)[PP], int t)
+template <int PP, int NT = RP_NT>
+__device__ __forceinline__ void rp_pub(const RX<PP> &X, int j, const Pr (&x)[rp_r(PP, NT)], int t)
 {
 #pragma unroll
-    for (int r = 0; r < PP; ++r) {
-        const int pp = t + RP_NT * r;
+    for (int r = 0; r < rp_r(PP, NT); ++r) {
+        const int pp = t + NT * r;
         *(rp_v4u *)(X.f(j) + 2 * pp) = pr_words(x[r]);
         X.h(j)[pp] = (short)x[r].h;
     }
@@ -229,38 +229,45 @@ __device__ __forceinline__ u32 rp_tw(const PassArgs &a, const BGeo &g, int li, i
     return (u32)(g.pos0 & (h - 1)) * unit + (u32)(k & ((1 << JB) - 1)) * (u32)g.pstep * unit;
 }
 
-// DIF pending exponent of slot s after `done` levels (bp_pend without the MFA twiddle
-// term: rp applies that on load)
-template <int LOGG>
-__device__ __forceinline__ u32 rp_pend(const PassArgs &a, const BGeo &g, int done, int s, u32 N2)
+// DIF pending exponent of position p after levels [lo, hi) of a length-2^lbM transform with
+// root 2^rho (in-place DIF: the bottom element of a level-lev butterfly takes the top one's
+// pending exponent plus the twiddle rho 2^lev (p mod h); the later levels' bits are the top's,
+// so every term is rho 2^lev (p mod 2^(lbM - hi)) -- each below N)
+__device__ __forceinline__ u32 rp_pend_pos(u32 rho, int lbM, int lo, int hi, u32 p, u32 N2)
 {
+    const u32 xm = p & ((1u << (lbM - hi)) - 1);
     u32 e = 0;
-    for (int j = 0; j < done; ++j)
-        if ((s >> (LOGG - 1 - j)) & 1) {
-            const int x = s & ~(((1 << (done - 1 - j)) - 1) << (LOGG - done));
-            e = rp_mod2n(e + rp_tw<LOGG, 0>(a, g, j, x), N2);
-        }
+    for (int lev = lo; lev < hi; ++lev)
+        if ((p >> (lbM - lev - 1)) & 1) e = rp_mod2n(e + (rho << lev) * xm, N2);
     return e;
 }
 
+// DIF pending exponent of slot s after `done` levels of this pass, including the levels an
+// earlier pass left pending (pcarry; bp_pend without the MFA twiddle term: rp applies that on load)
+template <int LOGG>
+__device__ __forceinline__ u32 rp_pend(const PassArgs &a, const BGeo &g, int done, int s, u32 N2)
+{
+    return rp_pend_pos((u32)a.rho, a.lbM, a.lvl0 - a.pcarry, a.lvl0 + done, (u32)(g.pos0 + s * g.pstep), N2);
+}
+
 // x_i <- 2^E(i) x_i for all G slots (general exponents), NX slots per LDS round
-template <int G, int PP, int NX, typename EF>
-__device__ __forceinline__ void rp_rot_all(Pr (&x)[G][PP], const RX<PP> &X, EF efn, u32 N, int t)
+template <int G, int PP, int NX, int NT = RP_NT, typename EF>
+__device__ __forceinline__ void rp_rot_all(Pr (&x)[G][rp_r(PP, NT)], const RX<PP> &X, EF efn, u32 N, int t)
 {
     t = rp_launder(t);
 #pragma unroll
     for (int i0 = 0; i0 < G; i0 += NX) {
 #pragma unroll
-        for (int q = 0; q < NX && i0 + q < G; ++q) rp_pub<PP>(X, q, x[i0 + q], t);
+        for (int q = 0; q < NX && i0 + q < G; ++q) rp_pub<PP, NT>(X, q, x[i0 + q], t);
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < NX && i0 + q < G; ++q) {
             const u32 e = efn(i0 + q);
             if (e == 0) continue;   // workgroup-uniform
 #pragma unroll
-            for (int r = 0; r < PP; ++r) {
+            for (int r = 0; r < rp_r(PP, NT); ++r) {
                 RP_FENCE();   // one pair position at a time (VGPRs)
-                x[i0 + q][r] = rp_get_gen<PP>(X, q, t + RP_NT * r, e, N);
+                x[i0 + q][r] = rp_get_gen<PP>(X, q, t + NT * r, e, N);
             }
         }
         __syncthreads();
@@ -274,12 +281,12 @@ __device__ __forceinline__ void rp_rot_all(Pr (&x)[G][PP], const RX<PP> &X, EF e
 // pending exponent of each slot after the last DIF level (applied by one aligned
 // rotation round); then G/2 partner exponents per level at 2G + li G/2.
 template <int LOGG, int DIR, bool GX>
-__device__ __forceinline__ u32 rp_exp_entry(const PassArgs &a, const BGeo &g, int e, u32 N2)
+__device__ __forceinline__ u32 rp_exp_entry(const PassArgs &a, const BGeo &g, int e, u32 N2, u32 cadd)
 {
     constexpr int G = 1 << LOGG;
     if (e < G) {
         if (!GX) return 0;
-        return DIR == 0 ? (u32)bp_mod2n(g.tw0 + (u64)e * g.twst, N2) : (u32)bp_post(a, g, e, N2);
+        return DIR == 0 ? (u32)bp_mod2n(g.tw0 + (u64)e * g.twst + cadd, N2) : (u32)bp_post(a, g, e, N2);
     }
     if (e < 2 * G) return DIR == 0 ? rp_pend<LOGG>(a, g, LOGG, e - G, N2) : 0;
     e -= 2 * G;
@@ -298,25 +305,25 @@ __device__ __forceinline__ u32 rp_exp_entry(const PassArgs &a, const BGeo &g, in
 
 
 // x_i <- 2^E(i) x_i for all G slots, every E a whole number of limb pairs
-template <int G, int PP, int NX, typename EF>
-__device__ __forceinline__ void rp_rot_all_al(Pr (&x)[G][PP], const RX<PP> &X, EF efn, u32 N, int t)
+template <int G, int PP, int NX, int NT = RP_NT, typename EF>
+__device__ __forceinline__ void rp_rot_all_al(Pr (&x)[G][rp_r(PP, NT)], const RX<PP> &X, EF efn, u32 N, int t)
 {
     t = rp_launder(t);
 #pragma unroll
     for (int i0 = 0; i0 < G; i0 += NX) {
 #pragma unroll
         for (int q = 0; q < NX && i0 + q < G; ++q)
-            if (efn(i0 + q)) rp_pub<PP>(X, q, x[i0 + q], t);   // uniform: slot 0 (e = 0) stays put
+            if (efn(i0 + q)) rp_pub<PP, NT>(X, q, x[i0 + q], t);   // uniform: slot 0 (e = 0) stays put
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < NX && i0 + q < G; ++q) {
             const u32 e = efn(i0 + q);
             if (e == 0) continue;
 #pragma unroll
-            for (int r = 0; r < PP; ++r) {
+            for (int r = 0; r < rp_r(PP, NT); ++r) {
                 RP_FENCE();
                 bool ng;
-                const Pr y = rp_get_al<PP>(X, q, t + RP_NT * r, e, N, ng);
+                const Pr y = rp_get_al<PP>(X, q, t + NT * r, e, N, ng);
                 x[i0 + q][r] = pr_cneg(y, ng);
             }
         }
@@ -359,32 +366,32 @@ __device__ __forceinline__ void rp_stage_codes(unsigned short *CODE, const Coef 
 }
 
 // limbs of the first NS slots (slot i at the uniform index SL[i])
-template <int NS, int NSX, int PP>
-__device__ __forceinline__ void rp_load_limbs(Pr (&x)[NSX][PP], const Coef &st, const u32 *SL, int t)
+template <int NS, int NSX, int PP, int NT = RP_NT>
+__device__ __forceinline__ void rp_load_limbs(Pr (&x)[NSX][rp_r(PP, NT)], const Coef &st, const u32 *SL, int t)
 {
     constexpr int l = 1024 * PP;
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
         const long sl = (long)rp_uniform(SL[i]);
 #pragma unroll
-        for (int r = 0; r < PP; ++r)
-            x[i][r] = pr_make(*(const rp_v4u *)(st.dig + (size_t)sl * l + 2 * (t + RP_NT * r)), 0);
+        for (int r = 0; r < rp_r(PP, NT); ++r)
+            x[i][r] = pr_make(*(const rp_v4u *)(st.dig + (size_t)sl * l + 2 * (t + NT * r)), 0);
     }
 }
 
 // codes -> pair form: limb 2pp's carry moves into limb 2pp+1, limb 2pp+1's (and the carry
 // limb) is the pair overflow h.  Ends with a barrier: CODE aliases the exchange slots.
-template <int NS, int NSX, int PP>
-__device__ __forceinline__ void rp_decode(Pr (&x)[NSX][PP], const unsigned short *CODE, int t)
+template <int NS, int NSX, int PP, int NT = RP_NT>
+__device__ __forceinline__ void rp_decode(Pr (&x)[NSX][rp_r(PP, NT)], const unsigned short *CODE, int t)
 {
     constexpr int HP = 512 * PP;
     t = rp_launder(t);
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
 #pragma unroll
-        for (int r = 0; r < PP; ++r) {
+        for (int r = 0; r < rp_r(PP, NT); ++r) {
             RP_FENCE();   // one code read at a time (else all are hoisted: VGPRs)
-            const int code = CODE[i * HP + t + RP_NT * r];
+            const int code = CODE[i * HP + t + NT * r];
             const int c0 = (signed char)(code & 0xff), c1 = (signed char)(code >> 8);
             int cc;   // b += c0 (branch-free: divergent branches here cost the allocator dearly)
             add_small(x[i][r].w[2], x[i][r].w[3], c0, cc);
@@ -398,15 +405,15 @@ __device__ __forceinline__ void rp_decode(Pr (&x)[NSX][PP], const unsigned short
 // exchange slots: callers end their last LDS phase with a barrier), then limb 2pp takes the
 // overflow of pair pp - 1 (pair 0: minus the last pair's, 2^N == -1); its carry out goes
 // into the masks, limb 2pp+1 carries 0
-template <int NS, int NSX, int PP, typename KEEP>
-__device__ __forceinline__ void rp_store(Pr (&x)[NSX][PP], const Coef &st, const u32 *SL, KEEP keep, short *HX, int t)
+template <int NS, int NSX, int PP, int NT = RP_NT, typename KEEP>
+__device__ __forceinline__ void rp_store(Pr (&x)[NSX][rp_r(PP, NT)], const Coef &st, const u32 *SL, KEEP keep, short *HX, int t)
 {
-    constexpr int l = 1024 * PP, HP = l / 2, cbw = 2 * l / 64;
+    constexpr int l = 1024 * PP, HP = l / 2, cbw = 2 * l / 64, R = rp_r(PP, NT);
     t = rp_launder(t);
 #pragma unroll
     for (int i = 0; i < NS; ++i)
 #pragma unroll
-        for (int r = 0; r < PP; ++r) HX[i * HP + t + RP_NT * r] = (short)x[i][r].h;
+        for (int r = 0; r < R; ++r) HX[i * HP + t + NT * r] = (short)x[i][r].h;
     __syncthreads();
     const int lane = t & 63, wv = t >> 6;
 #pragma unroll
@@ -416,34 +423,43 @@ __device__ __forceinline__ void rp_store(Pr (&x)[NSX][PP], const Coef &st, const
         u64 *dst = st.dig + (size_t)sl * l;
         u64 *cbp = st.cb + (size_t)sl * cbw;
 #pragma unroll
-        for (int r = 0; r < PP; ++r) {
+        for (int r = 0; r < R; ++r) {
             RP_FENCE();
-            const int pp = t + RP_NT * r;
+            const int pp = t + NT * r;
             const int hv = HX[i * HP + (pp ? pp - 1 : HP - 1)];
             const int hin = pp ? hv : -hv;
             int k0;
             add_small(x[i][r].w[0], x[i][r].w[1], hin, k0);
             *(rp_v4u *)(dst + 2 * pp) = pr_words(x[i][r]);
-            // mask words of rows 2 (wv + 8r) (pairs of lanes 0..31) and +1 (lanes 32..63): bit 2j
+            // mask words of rows 2 (wv + NW r) (NW = NT / 64 waves; pairs of lanes 0..31) and +1 (lanes 32..63): bit 2j
             // is pair j's even limb (odd limbs carry nothing).  Lane L fetches the carry of pair
-            // L/2 (resp. 32 + L/2), so one ballot over the even lanes is the word.
+            // L/2 (resp. 32 + L/2), so one ballot over the even lanes is the word.  (One ballot
+            // per sign spread to the even bits on the scalar unit measured slower: ~60 SALU
+            // instructions per word pair against two lane shuffles.)
             const int ka = __shfl(k0, lane >> 1), kb = __shfl(k0, 32 + (lane >> 1));
             const bool ev = !(lane & 1);
             const u64 pa = __ballot(ev && ka == 1), na = __ballot(ev && ka == -1);
             const u64 pb = __ballot(ev && kb == 1), nb = __ballot(ev && kb == -1);
             if (lane < 2)
-                *(rp_v2u *)(cbp + 2 * (2 * (wv + 8 * r) + lane)) = lane ? rp_v2u{pb, nb} : rp_v2u{pa, na};
+                *(rp_v2u *)(cbp + 2 * (2 * (wv + (NT / 64) * r) + lane)) = lane ? rp_v2u{pb, nb} : rp_v2u{pa, na};
         }
         if (t == 0) st.top[sl] = 0;
     }
 }
 
-// MODE: DIR 0: 0 plain, 1 MFA twiddle on load, 2 split on load (first column pass);
-//       DIR 1: 0 plain, 1 general final multipliers (inverse twiddle / scaling)
+// MODE: DIR 0: 0 plain, 1 MFA twiddle on load, 2 split on load (first column pass),
+//               3 plain with inputs that still owe an earlier pass's pending exponents
+//               (PassArgs::pcarry: the first level rotates its partners through LDS too);
+//       DIR 1: bit 0 general final multipliers (inverse twiddle / scaling), bit 1 the pass
+//               holds the transform's last DIT level (h = 1: its first level needs no rotation)
+// (compile-time, so the register-only level and the LDS level are never both in one kernel:
+// a runtime choice between them spilled)
 template <int LOGG, int PP, int DIR, int MODE>
-__global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
+__global__ __launch_bounds__(rp_nt(1024 * PP, LOGG), 4) void k_rpass(PassArgs a)
 {
-    constexpr bool GX = MODE == 1, SPLIT = DIR == 0 && MODE == 2;
+    constexpr int NT = rp_nt(1024 * PP, LOGG), R = rp_r(PP, NT);
+    constexpr bool GX = DIR == 0 ? MODE == 1 : (MODE & 1) != 0, SPLIT = DIR == 0 && MODE == 2,
+                   CIN = DIR == 0 && MODE == 3, HL = DIR == 1 && (MODE & 2) != 0;
     pass_clear_flags(a);
     constexpr int G = 1 << LOGG, NX = G / 2 > 2 ? G / 2 : 2;
     constexpr int l = 1024 * PP, HP = l / 2, cbw = 2 * l / 64;
@@ -484,7 +500,12 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
     constexpr int NEXP = 2 * G + (G / 2) * LOGG;
     u32 *EXPT = (u32 *)(smem + NX * RX<PP>::SB);
     u32 *SLT = EXPT + NEXP;
-    if (t < NEXP) EXPT[t] = rp_exp_entry<LOGG, DIR, GX>(a, g, t, N2);
+    // first row pass after columns that kept their pending exponents: the row's column pending
+    // exponent (physical row = column-transform position) joins the MFA twiddle (uniform)
+    const u32 cadd = DIR == 0 && GX && a.ccarry
+                         ? rp_pend_pos((u32)(a.tw_w << a.lbM), a.tw_lbR, a.tw_lbR - a.ccarry, a.tw_lbR, (u32)(a.sub_off + sub), N2)
+                         : 0u;
+    if (t < NEXP) EXPT[t] = rp_exp_entry<LOGG, DIR, GX>(a, g, t, N2, cadd);
     else if (t < NEXP + G) SLT[t - NEXP] = (u32)slot_lane(t - NEXP);
     __syncthreads();
     const u64 *src = SPLIT ? a.src[op] : nullptr;
@@ -495,20 +516,20 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
 
     // ---- load ------------------------------------------------------------------------
     unsigned short *CODE = (unsigned short *)smem;   // G HP codes (over the exchange slots)
-    Pr x[G][PP];
+    Pr x[G][R];
     if (!SPLIT) {
         rp_stage_codes<G, PP>(CODE, st, SLT, t);
-        rp_load_limbs<G, G, PP>(x, st, SLT, t);
+        rp_load_limbs<G, G, PP, NT>(x, st, SLT, t);
         __syncthreads();
-        rp_decode<G, G, PP>(x, CODE, t);
+        rp_decode<G, G, PP, NT>(x, CODE, t);
     } else {   // first forward column pass: FFT_split_bits fused into the load
 #pragma unroll
         for (int i = 0; i < G; ++i) {
             __builtin_amdgcn_sched_barrier(0);   // 3 source limbs per pair, a slot at a time
             const bool z = zero_in(i);
 #pragma unroll
-            for (int r = 0; r < PP; ++r) {
-                const int pp = t + RP_NT * r;
+            for (int r = 0; r < R; ++r) {
+                const int pp = t + NT * r;
                 x[i][r] = Pr{{0, 0, 0, 0}, 0};
                 if (z) continue;
                 const u64 left = (u64)pp * 128 < a.bits1 ? a.bits1 - (u64)pp * 128 : 0;   // bits of the coefficient here
@@ -530,7 +551,7 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
     }
     RP_STAMP(1);
     if (DIR == 0 && GX) {   // MFA twiddle 2^(tw0 + s twst) of slot s (README:89), so every level is pair-aligned
-        rp_rot_all<G, PP, NX>(x, X, [&](int s) -> u32 { return rp_uniform(EXPT[s]); }, N, t);
+        rp_rot_all<G, PP, NX, NT>(x, X, [&](int s) -> u32 { return rp_uniform(EXPT[s]); }, N, t);
     }
 
     // ---- levels ----------------------------------------------------------------------
@@ -538,16 +559,16 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
     for (int li = 0; li < LOGG; ++li) {
         const int JB = DIR == 0 ? LOGG - 1 - li : li;
         // E == 0 for every pair of the level: the first DIF level of a pass (no pending
-        // exponents yet, rp_pend(.., 0, ..) == 0) and the first DIT level of the pass that holds
-        // the transform's last level (h == 1: rp_tw == 0).  Partners are then this thread's own
-        // registers -- no LDS round (workgroup-uniform condition).
-        if ((DIR == 0 && li == 0) || (DIR == 1 && li == 0 && a.lvl0 + LOGG == a.lbM)) {
+        // exponents yet, rp_pend(.., 0, ..) == 0, unless an earlier pass left its own) and the
+        // first DIT level of the pass that holds the transform's last level (h == 1: rp_tw == 0).
+        // Partners are then this thread's own registers -- no LDS round (workgroup-uniform).
+        if ((DIR == 0 && li == 0 && !CIN) || (DIR == 1 && li == 0 && HL)) {
 #pragma unroll
             for (int pi = 0; pi < G / 2; ++pi) {
                 const int i = ((pi >> JB) << (JB + 1)) | (pi & ((1 << JB) - 1));
                 const int k = i | (1 << JB);
 #pragma unroll
-                for (int r = 0; r < PP; ++r) {
+                for (int r = 0; r < R; ++r) {
                     const Pr y = x[k][r];
                     pr_bfly(x[i][r], x[k][r], x[i][r], y, false);
                 }
@@ -560,7 +581,7 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
 #pragma unroll
         for (int pi = 0; pi < G / 2; ++pi) {
             const int i = ((pi >> JB) << (JB + 1)) | (pi & ((1 << JB) - 1));
-            rp_pub<PP>(X, pi, x[i | (1 << JB)], tl);
+            rp_pub<PP, NT>(X, pi, x[i | (1 << JB)], tl);
         }
         __syncthreads();
 #pragma unroll
@@ -569,26 +590,26 @@ __global__ __launch_bounds__(RP_NT, 4) void k_rpass(PassArgs a)
             const int k = i | (1 << JB);
             const u32 E = rp_uniform(EXPT[2 * G + (G / 2) * li + pi]);
 #pragma unroll
-            for (int r = 0; r < PP; ++r) {
+            for (int r = 0; r < R; ++r) {
                 if (r % 2 == 0) RP_FENCE();   // two partner reads in flight at a time
                 bool ng;
-                const Pr y = rp_get_al<PP>(X, pi, tl + RP_NT * r, E, N, ng);
+                const Pr y = rp_get_al<PP>(X, pi, tl + NT * r, E, N, ng);
                 pr_bfly(x[i][r], x[k][r], x[i][r], y, ng);
             }
         }
         __syncthreads();
         if (li < 3) RP_STAMP(2 + li);
     }
-    if (DIR == 0) {   // the pending exponents of the last level (whole pairs): one aligned rotation round
-        rp_rot_all_al<G, PP, NX>(x, X, [&](int s) -> u32 { return rp_uniform(EXPT[G + s]); }, N, t);
+    if (DIR == 0 && !a.pkeep) {   // the pending exponents of the last level (whole pairs): one aligned rotation round
+        rp_rot_all_al<G, PP, NX, NT>(x, X, [&](int s) -> u32 { return rp_uniform(EXPT[G + s]); }, N, t);
     }
     if (DIR == 1 && GX) {   // inverse MFA twiddle and/or fused scaling (bp_post)
-        rp_rot_all<G, PP, NX>(x, X, [&](int s) -> u32 { return rp_uniform(EXPT[s]); }, N, t);
+        rp_rot_all<G, PP, NX, NT>(x, X, [&](int s) -> u32 { return rp_uniform(EXPT[s]); }, N, t);
     }
     RP_STAMP(5);
 
     // ---- store (reduced form) --------------------------------------------------------
-    rp_store<G, G, PP>(x, st, SLT, [&](int i) -> bool {
+    rp_store<G, G, PP, NT>(x, st, SLT, [&](int i) -> bool {
         return DIR == 1 || ((g.pos0 + i * g.pstep) & ~(g.pstep - 1)) < a.need;
     }, (short *)smem, t);
     RP_STAMP(6);

@@ -3,19 +3,21 @@
 
 rp_fn rp_get_p1(int logg, int dir, int mode)
 {
-    static const rp_fn tab[2][3][4] = {
+    static const rp_fn tab[2][4][4] = {
         {
             {nullptr, k_rpass<1, 1, 0, 0>, k_rpass<2, 1, 0, 0>, k_rpass<3, 1, 0, 0>},
             {nullptr, k_rpass<1, 1, 0, 1>, k_rpass<2, 1, 0, 1>, k_rpass<3, 1, 0, 1>},
             {nullptr, k_rpass<1, 1, 0, 2>, k_rpass<2, 1, 0, 2>, k_rpass<3, 1, 0, 2>},
+            {nullptr, k_rpass<1, 1, 0, 3>, k_rpass<2, 1, 0, 3>, k_rpass<3, 1, 0, 3>},
         },
         {
             {nullptr, k_rpass<1, 1, 1, 0>, k_rpass<2, 1, 1, 0>, k_rpass<3, 1, 1, 0>},
             {nullptr, k_rpass<1, 1, 1, 1>, k_rpass<2, 1, 1, 1>, k_rpass<3, 1, 1, 1>},
-            {nullptr, nullptr, nullptr, nullptr},
+            {nullptr, k_rpass<1, 1, 1, 2>, k_rpass<2, 1, 1, 2>, k_rpass<3, 1, 1, 2>},
+            {nullptr, k_rpass<1, 1, 1, 3>, k_rpass<2, 1, 1, 3>, k_rpass<3, 1, 1, 3>},
         },
     };
-    if (logg < 1 || logg > 3 || dir < 0 || dir > 1 || mode < 0 || mode > 2) return nullptr;
+    if (logg < 1 || logg > 3 || dir < 0 || dir > 1 || mode < 0 || mode > 3) return nullptr;
     return tab[dir][mode][logg];
 }
 
