@@ -311,7 +311,11 @@ struct Exec {
     int in_rows = 0;         // non-zero: inputs live in column rows [0, in_rows) (default: the trunc rows)
     bool defer_double = false;   // itft's top-level doubling is left to scale() (rows [dbl_lo, dbl_hi): 2^-depth)
     bool fuse_row_last = false;  // the row DIF's last level runs inside the pointwise (k_pwss PAIR)
-    bool carry_pend = false;     // forward k_rpass passes hand their pending exponents on (fwd_columns)
+    // forward k_rpass passes hand their pending exponents on (fwd_columns / fwd_rows).  Every
+    // stage still ends exact: a transform's last level leaves no pending exponent, and the last
+    // row pass (before the pointwise) never hands on -- so the stage API and the sharded path
+    // use it too.
+    bool carry_pend = !diag_env("MPFFT_NO_CARRY");
     // which hand-overs: 1 column -> column, 2 last column -> first row (its MFA twiddle rotation
     // absorbs them; a no-op in practice: after a transform's last level every DIF pending
     // exponent is 0), 4 row -> row.  A hand-over into a plain pass moves that pass's first level
@@ -597,7 +601,7 @@ struct Exec {
         return a;
     }
 
-    // Pending exponents across forward passes (carry_pend, single-GPU run_all / run_all6): a
+    // Pending exponents across forward passes (carry_pend): a
     // k_rpass DIF pass whose successor is also a k_rpass DIF pass skips its closing rotation
     // round (the last level's pending exponents, one LDS round trip of all G coefficients) and
     // leaves them in HBM; the successor folds them into its first level's partner rotations
@@ -1127,7 +1131,6 @@ static int run_all6(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, u
     X2.shift(2 * P.n);
     X2.in_rows = (int)P.NR;   // the second half's inputs are all live (FFT_radix2_truncate1_twiddle)
     X1.fuse_row_last = X2.fuse_row_last = true;   // each half's last row level inside its pointwise
-    X1.carry_pend = X2.carry_pend = !diag_env("MPFFT_NO_CARRY");
     XS.single(ws);
     XC.single(ws);
     const bool two = P2.Tr > 0;
@@ -1185,7 +1188,6 @@ static int run_all(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, un
     X.zflags_n = X.comb_flag_words(P.total);
     X.defer_double = true;   // itft + scale back to back
     X.fuse_row_last = true;  // last row level inside the pointwise (nested negacyclic sizes)
-    X.carry_pend = !diag_env("MPFFT_NO_CARRY");
     ProfCall pc;
     int rc;
     pc.mark(0, s);

@@ -97,7 +97,13 @@ class ShardedMul:
         self.sliced = sliced          # run() gets this rank's operand slices (ShardPlan.slice_operand)
         p = plan
         self.col = [backend.alloc_coeffs(p.col_slots()) for _ in range(2)]
-        self.row = [backend.alloc_coeffs(p.row_slots(rank)) for _ in range(2)]
+        if p.world == 1:
+            # one rank: the row layout (ccb = C = NC, rows [0, Tr)) is the column layout's first
+            # Tr NC slots, so the row arrays are views of the column arrays and the exchanges
+            # find nothing to move (no stage reads one layout while writing the other)
+            self.row = [{f: c[f][: p.row_slots(rank) * backend.width(f, p)] for f in c} for c in self.col]
+        else:
+            self.row = [backend.alloc_coeffs(p.row_slots(rank)) for _ in range(2)]
         # the row DIF's last level fused into the pointwise, as on one GPU: the product lands in
         # a third row array, which then serves as operand 0's row array (swapped after the stage)
         self.fused = bool(getattr(backend, "row_fused", lambda: False)())
@@ -178,6 +184,14 @@ class ShardedMul:
         return m0, limbs
 
 
+def _same_view(a, b):
+    """a and b are the same elements of the same buffer (a local exchange with nothing to move)."""
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr() == b.data_ptr() and a.numel() == b.numel() and a.dtype == b.dtype
+    return a is b or (getattr(a, "base", None) is not None and a.__array_interface__["data"] == b.__array_interface__["data"]
+                      and a.shape == b.shape)
+
+
 def torch_empty_like_cpu(t):
     import torch
     return torch.empty(t.shape, dtype=t.dtype)
@@ -206,7 +220,8 @@ class TorchComm:
         me = self.dist.get_rank()
         ops, back = [], []
         for send, recv in plan:
-            recv[me].copy_(send[me])
+            if not _same_view(recv[me], send[me]):
+                recv[me].copy_(send[me])
             for d in range(len(send)):
                 if d == me:
                     continue
@@ -438,7 +453,8 @@ class _SoloComm:
 
     def exchange(self, plan):
         for send, recv in plan:
-            recv[0].copy_(send[0])
+            if not _same_view(recv[0], send[0]):
+                recv[0].copy_(send[0])
 
     def all_to_all(self, out, inp, out_splits, in_splits):
         out[: inp.numel()].copy_(inp)

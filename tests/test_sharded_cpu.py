@@ -80,6 +80,7 @@ def _run(world, depth, w, n1, n2, seed=1):
     (2, 7, 1, 5, 4),       # trunc < 2n (van der Hoeven case a)
     (4, 8, 1, 100, 90),    # 4 ranks, truncated
     (2, 8, 2, 50, 3),      # unbalanced operands
+    (1, 7, 1, 5, 4),       # one rank: row arrays alias the column arrays, exchanges move nothing
 ])
 def test_sharded_gloo_exact(world, depth, w, n1, n2):
     _run(world, depth, w, n1, n2)
