@@ -58,6 +58,10 @@ struct PassArgs {
     int pkeep;           // leave every pending exponent in the output (the next pass applies them)
     int ccarry;          // first row pass (tw_mode 1): the input owes the column DIF's pending
                          // exponents of levels [tw_lbR - ccarry, tw_lbR) at its row
+    // the truncated inverse's FILL step folded into a block's last DIT pass (k_rpass DIR 1,
+    // mode bit 2): positions p >= fill_lo also store 2^(p fill_rho) x_p at position p + fill_off
+    int fill_lo, fill_off;
+    u64 fill_rho;
 };
 
 // Grid-stride clear of PassArgs::zp; called at the top of every pass kernel, before

@@ -328,6 +328,7 @@ struct Exec {
         return m >= 0 ? m : P.l >= 4096 ? 7 : 6;
     }
     int col_carry = 0;           // column levels whose pending exponents the first row pass applies
+    struct Fill { long lo = 0, off = 0; u64 rho = 0; bool done = false; } fill;   // itft's FILL, see ifft_block
     long dbl_lo = 0, dbl_hi = 0;
 
     Exec(const Plan &p, hipStream_t st) : P(p), s(st) { nw = P.tpb / 64; }
@@ -415,7 +416,9 @@ struct Exec {
             return a.pcarry ? 3 : 0;
         }
         if (a.tw_mode == 1) return -1;
-        return ((a.tw_mode == 2 || a.scale_e) ? 1 : 0) | (a.lvl0 + logg == a.lbM ? 2 : 0);
+        const int gx = (a.tw_mode == 2 || a.scale_e) ? 1 : 0;
+        if (a.fill_off && gx) return -1;
+        return gx | (a.lvl0 + logg == a.lbM ? 2 : 0) | (a.fill_off ? 4 : 0);
     }
 
     // the k_rpass mode pass() launches for these arguments, -1: another kernel family
@@ -842,6 +845,16 @@ struct Exec {
                 a.scale_e = 2 * P.N - (u64)(P.depth + 1);
                 a.canon = 1;
             }
+            if (hi - k == 0 && fill.off) {   // the block's last pass also does the pending FILL step
+                PassArgs f = a;
+                f.fill_lo = (int)fill.lo;
+                f.fill_off = (int)fill.off;
+                f.fill_rho = fill.rho;
+                if (rp_mode(f, k, 1) >= 0) {
+                    a = f;
+                    fill.done = true;
+                }
+            }
             int rc = pass(a, k, 1, 1);
             if (rc) return rc;
             hi -= k;
@@ -914,8 +927,12 @@ struct Exec {
             }
             return pairop(OP_DOUBLE, off, h, 0, t, 0);
         }
-        if ((rc = ifft_block(off, h))) return rc;
-        if ((rc = pairop(OP_FILL, off, h, t - h, h - (t - h), rho_blk(m)))) return rc;
+        fill = {t - h, h, rho_blk(m), false};   // offered to ifft_block's last pass
+        rc = ifft_block(off, h);
+        const bool filled = fill.done;
+        fill = {};
+        if (rc) return rc;
+        if (!filled && (rc = pairop(OP_FILL, off, h, t - h, h - (t - h), rho_blk(m)))) return rc;
         if ((rc = itft1(off + h, h, t - h))) return rc;
         if ((rc = pairop(OP_IBFLY, off, h, 0, t - h, rho_blk(m)))) return rc;
         if (top) {
@@ -949,13 +966,15 @@ struct Exec {
         if (P.fuse_scale) return MPFFT_OK;   // done by the last inverse column pass
         const u64 e = 2 * P.N - (u64)(P.depth + 1);
         if (dbl_hi <= dbl_lo) return scale_rows(0, P.Tr, e);
+        if (P.rpass) return scale_rows(0, P.Tr, e, dbl_lo, dbl_hi);   // one launch, two exponents
         int rc;
         if ((rc = scale_rows(0, dbl_lo, e))) return rc;
         if ((rc = scale_rows(dbl_lo, dbl_hi, e + 1))) return rc;
         return scale_rows(dbl_hi, P.Tr, e);
     }
 
-    int scale_rows(long r0_, long r1_, u64 e)
+    // rows [r0_, r1_) by 2^e; with rpass, rows [d0, d1) inside them by 2^(e+1)
+    int scale_rows(long r0_, long r1_, u64 e, long d0 = 0, long d1 = 0)
     {
         const long cnt = (r1_ - r0_) * ccount, s0 = r0_ * ccount;
         if (cnt <= 0) return MPFFT_OK;
@@ -964,8 +983,9 @@ struct Exec {
         if (P.rpass) {   // register-resident scale + canonicalisation (rkernels.hpp)
             rp_scale_fn f = rp_scale_get((int)P.l);
             if (!f) return MPFFT_EUNSUPPORTED;
+            const unsigned lo = (unsigned)((d0 - r0_) * ccount), hi = (unsigned)((d1 - r0_) * ccount);
             hipLaunchKernelGGL(f, dim3((unsigned)cnt), dim3(RP_NT), rp_scale_lds((int)P.l), s, dig, cbp, top, (unsigned)P.N,
-                               (unsigned)e);
+                               (unsigned)e, (unsigned)(e + 1), d1 > d0 ? lo : 0u, d1 > d0 ? hi : 0u);
             HIPCHK(hipGetLastError());
             return MPFFT_OK;
         }

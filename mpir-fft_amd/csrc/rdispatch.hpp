@@ -41,6 +41,6 @@ rp_pair_fn rp_pair_get(int l, int op);
 inline size_t rp_pair_lds(int l) { return (size_t)9 * l + 16; }
 
 // k_rscale<PP>: x <- 2^e x, canonical (the 2^-(depth+1) scaling before the combine)
-typedef void (*rp_scale_fn)(uint64_t *, uint64_t *, int *, unsigned, unsigned);
+typedef void (*rp_scale_fn)(uint64_t *, uint64_t *, int *, unsigned, unsigned, unsigned, unsigned, unsigned);
 rp_scale_fn rp_scale_get(int l);
 inline size_t rp_scale_lds(int l) { return (size_t)9 * l + (size_t)l + 128; }   // slot + pair overflows + canon scratch

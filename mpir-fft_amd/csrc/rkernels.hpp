@@ -406,7 +406,7 @@ __device__ __forceinline__ void rp_decode(Pr (&x)[NSX][rp_r(PP, NT)], const unsi
 // overflow of pair pp - 1 (pair 0: minus the last pair's, 2^N == -1); its carry out goes
 // into the masks, limb 2pp+1 carries 0
 template <int NS, int NSX, int PP, int NT = RP_NT, typename KEEP>
-__device__ __forceinline__ void rp_store(Pr (&x)[NSX][rp_r(PP, NT)], const Coef &st, const u32 *SL, KEEP keep, short *HX, int t)
+__device__ __forceinline__ void rp_store(const Pr (&x)[NSX][rp_r(PP, NT)], const Coef &st, const u32 *SL, KEEP keep, short *HX, int t)
 {
     constexpr int l = 1024 * PP, HP = l / 2, cbw = 2 * l / 64, R = rp_r(PP, NT);
     t = rp_launder(t);
@@ -429,8 +429,9 @@ __device__ __forceinline__ void rp_store(Pr (&x)[NSX][rp_r(PP, NT)], const Coef 
             const int hv = HX[i * HP + (pp ? pp - 1 : HP - 1)];
             const int hin = pp ? hv : -hv;
             int k0;
-            add_small(x[i][r].w[0], x[i][r].w[1], hin, k0);
-            *(rp_v4u *)(dst + 2 * pp) = pr_words(x[i][r]);
+            u32 w0 = x[i][r].w[0], w1 = x[i][r].w[1];   // x itself stays intact (k_rpass FILL stores it twice)
+            add_small(w0, w1, hin, k0);
+            *(rp_v4u *)(dst + 2 * pp) = rp_v4u{w0, w1, x[i][r].w[2], x[i][r].w[3]};
             // mask words of rows 2 (wv + NW r) (NW = NT / 64 waves; pairs of lanes 0..31) and +1 (lanes 32..63): bit 2j
             // is pair j's even limb (odd limbs carry nothing).  Lane L fetches the carry of pair
             // L/2 (resp. 32 + L/2), so one ballot over the even lanes is the word.  (One ballot
@@ -451,7 +452,8 @@ __device__ __forceinline__ void rp_store(Pr (&x)[NSX][rp_r(PP, NT)], const Coef 
 //               3 plain with inputs that still owe an earlier pass's pending exponents
 //               (PassArgs::pcarry: the first level rotates its partners through LDS too);
 //       DIR 1: bit 0 general final multipliers (inverse twiddle / scaling), bit 1 the pass
-//               holds the transform's last DIT level (h = 1: its first level needs no rotation)
+//               holds the transform's last DIT level (h = 1: its first level needs no rotation),
+//               bit 2 the truncated inverse's FILL step (PassArgs::fill_*; not with bit 0)
 // (compile-time, so the register-only level and the LDS level are never both in one kernel:
 // a runtime choice between them spilled)
 template <int LOGG, int PP, int DIR, int MODE>
@@ -459,7 +461,8 @@ __global__ __launch_bounds__(rp_nt(1024 * PP, LOGG), 4) void k_rpass(PassArgs a)
 {
     constexpr int NT = rp_nt(1024 * PP, LOGG), R = rp_r(PP, NT);
     constexpr bool GX = DIR == 0 ? MODE == 1 : (MODE & 1) != 0, SPLIT = DIR == 0 && MODE == 2,
-                   CIN = DIR == 0 && MODE == 3, HL = DIR == 1 && (MODE & 2) != 0;
+                   CIN = DIR == 0 && MODE == 3, HL = DIR == 1 && (MODE & 2) != 0,
+                   FILL = DIR == 1 && (MODE & 4) != 0;
     pass_clear_flags(a);
     constexpr int G = 1 << LOGG, NX = G / 2 > 2 ? G / 2 : 2;
     constexpr int l = 1024 * PP, HP = l / 2, cbw = 2 * l / 64;
@@ -612,6 +615,15 @@ __global__ __launch_bounds__(rp_nt(1024 * PP, LOGG), 4) void k_rpass(PassArgs a)
     rp_store<G, G, PP, NT>(x, st, SLT, [&](int i) -> bool {
         return DIR == 1 || ((g.pos0 + i * g.pstep) & ~(g.pstep - 1)) < a.need;
     }, (short *)smem, t);
+    if (FILL) {   // IFFT_radix2_truncate's fill (mul_fft.c:1760-1764): b_(p+h) = 2^(p rho) a_p for p >= t - h
+        auto fills = [&](int s) -> bool { return g.pos0 + s * g.pstep >= a.fill_lo; };
+        __syncthreads();   // every HX read of the store done (the rotation reuses the exchange slots)
+        if (t < G) SLT[t] += (u32)((long)a.fill_off * a.pos_stride);
+        rp_rot_all_al<G, PP, NX, NT>(x, X, [&](int s) -> u32 {
+            return fills(s) ? (u32)(((u64)(g.pos0 + s * g.pstep) * a.fill_rho) % N2) : 0u;
+        }, N, t);
+        rp_store<G, G, PP, NT>(x, st, SLT, fills, (short *)smem, t);
+    }
     RP_STAMP(6);
     if (stamp) {
         __syncthreads();
@@ -831,9 +843,11 @@ __device__ int rp_canon_par(const BSlot &b, int l, int wave, int lane, int *scr)
 // slot form (limb + carry into it) and the rows are swept (the ballot carry-lookahead of
 // mpn_normmod_2expp1 :272) by all eight waves, one segment each (rp_canon_par);
 // the canonical residue in [0, 2^N] is stored with zero carry masks and its carry limb.
+// Coefficients [lo, hi) of the launch take exponent e2 instead of e (one launch for all rows).
 template <int PP>
-__global__ __launch_bounds__(RP_NT) void k_rscale(u64 *dig, u64 *cb, int *top, u32 N, u32 e)
+__global__ __launch_bounds__(RP_NT) void k_rscale(u64 *dig, u64 *cb, int *top, u32 N, u32 e, u32 e2, u32 lo, u32 hi)
 {
+    if (blockIdx.x >= lo && blockIdx.x < hi) e = e2;   // itft's deferred doubling: those rows by 2^-depth
     constexpr int l = 1024 * PP, HP = l / 2, cbw = 2 * l / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const RX<PP> X{smem};

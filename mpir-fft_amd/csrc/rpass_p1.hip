@@ -3,21 +3,26 @@
 
 rp_fn rp_get_p1(int logg, int dir, int mode)
 {
-    static const rp_fn tab[2][4][4] = {
+    static const rp_fn tab[2][8][4] = {
         {
             {nullptr, k_rpass<1, 1, 0, 0>, k_rpass<2, 1, 0, 0>, k_rpass<3, 1, 0, 0>},
             {nullptr, k_rpass<1, 1, 0, 1>, k_rpass<2, 1, 0, 1>, k_rpass<3, 1, 0, 1>},
             {nullptr, k_rpass<1, 1, 0, 2>, k_rpass<2, 1, 0, 2>, k_rpass<3, 1, 0, 2>},
             {nullptr, k_rpass<1, 1, 0, 3>, k_rpass<2, 1, 0, 3>, k_rpass<3, 1, 0, 3>},
+            {}, {}, {}, {},
         },
         {
             {nullptr, k_rpass<1, 1, 1, 0>, k_rpass<2, 1, 1, 0>, k_rpass<3, 1, 1, 0>},
             {nullptr, k_rpass<1, 1, 1, 1>, k_rpass<2, 1, 1, 1>, k_rpass<3, 1, 1, 1>},
             {nullptr, k_rpass<1, 1, 1, 2>, k_rpass<2, 1, 1, 2>, k_rpass<3, 1, 1, 2>},
             {nullptr, k_rpass<1, 1, 1, 3>, k_rpass<2, 1, 1, 3>, k_rpass<3, 1, 1, 3>},
+            {nullptr, k_rpass<1, 1, 1, 4>, k_rpass<2, 1, 1, 4>, k_rpass<3, 1, 1, 4>},
+            {nullptr, nullptr, nullptr, nullptr},
+            {nullptr, k_rpass<1, 1, 1, 6>, k_rpass<2, 1, 1, 6>, k_rpass<3, 1, 1, 6>},
+            {nullptr, nullptr, nullptr, nullptr},
         },
     };
-    if (logg < 1 || logg > 3 || dir < 0 || dir > 1 || mode < 0 || mode > 3) return nullptr;
+    if (logg < 1 || logg > 3 || dir < 0 || dir > 1 || mode < 0 || mode > 7) return nullptr;
     return tab[dir][mode][logg];
 }
 
@@ -54,10 +59,10 @@ rp_pair_fn rp_pair_get(int l, int op)
     return nullptr;
 }
 
-void (*rp_scale_get_p1())(u64 *, u64 *, int *, u32, u32) { return k_rscale<1>; }
+void (*rp_scale_get_p1())(u64 *, u64 *, int *, u32, u32, u32, u32, u32) { return k_rscale<1>; }
 
-void (*rp_scale_get_p2())(u64 *, u64 *, int *, u32, u32);
-void (*rp_scale_get_p4())(u64 *, u64 *, int *, u32, u32);
+void (*rp_scale_get_p2())(u64 *, u64 *, int *, u32, u32, u32, u32, u32);
+void (*rp_scale_get_p4())(u64 *, u64 *, int *, u32, u32, u32, u32, u32);
 
 rp_scale_fn rp_scale_get(int l)
 {
