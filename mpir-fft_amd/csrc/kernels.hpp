@@ -288,6 +288,7 @@ struct PairArgs {
     int ncol;
     int off, h, i0, cnt;
     u64 rho;      // e_i = i * rho (mod 2N)
+    int nb, hb[3], xoff;   // k_rchain: TWOXMY partner offsets, the enclosing IBFLY's top rows
 };
 
 template <int U>

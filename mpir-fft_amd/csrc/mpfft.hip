@@ -830,6 +830,7 @@ struct Exec {
     // full inverse (DIT) over block [off, off + m) of every local column
     int ifft_block(long off, long m)
     {
+        if (int rc = flush_chain()) return rc;
         const int lbM = ilog2(m);
         int hi = lbM;
         while (hi > 0) {
@@ -862,7 +863,72 @@ struct Exec {
         return MPFFT_OK;
     }
 
+    // The truncated inverse's tail (Exec::chain): TWOXMY steps on one row range are held back
+    // and run together with the IBFLY that consumes their rows (k_rchain), so those rows are
+    // read once; anything else flushes them first.
+    struct Chain { long off = 0, t = 0; int n = 0; long h[3] = {0, 0, 0}; } chain;
+
+    int flush_chain()
+    {
+        const Chain c = chain;
+        chain.n = 0;
+        for (int j = 0; j < c.n; ++j) {
+            int rc = pairop_now(OP_TWOXMY, c.off, c.h[j], 0, c.t, 0);
+            if (rc) return rc;
+        }
+        return MPFFT_OK;
+    }
+
+    PairArgs pair_args(int op, long off, long h, long i0, long cnt, u64 rho) const
+    {
+        PairArgs a;
+        memset(&a, 0, sizeof(a));
+        a.dig = col.dig[0];
+        a.cb = col.cb[0];
+        a.top = col.top[0];
+        a.N = P.N;
+        a.l = (int)P.l;
+        a.op = op;
+        a.NC = ccount;
+        a.ncol = ccount;
+        a.off = (int)off;
+        a.h = (int)h;
+        a.i0 = (int)i0;
+        a.cnt = (int)cnt;
+        a.rho = rho;
+        return a;
+    }
+
     int pairop(int op, long off, long h, long i0, long cnt, u64 rho)
+    {
+        if (cnt <= 0) return MPFFT_OK;
+        int rc;
+        const bool chains = P.rpass && rp_chain_get((int)P.l, 1) && !diag_env("MPFFT_NO_CHAIN");
+        if (chains && op == OP_TWOXMY && i0 == 0) {
+            if (chain.n && (chain.off != off || chain.t != cnt || chain.n == 3) && (rc = flush_chain())) return rc;
+            if (!chain.n) {
+                chain.off = off;
+                chain.t = cnt;
+            }
+            chain.h[chain.n++] = h;
+            return MPFFT_OK;
+        }
+        if (chains && op == OP_IBFLY && i0 == 0 && chain.n && chain.off == off + h && chain.t == cnt) {
+            PairArgs a = pair_args(op, off + h, h, 0, cnt, rho);
+            a.nb = chain.n;
+            for (int j = 0; j < chain.n; ++j) a.hb[j] = (int)chain.h[j];
+            a.xoff = (int)off;
+            rp_pair_fn f = rp_chain_get((int)P.l, chain.n);
+            chain.n = 0;
+            hipLaunchKernelGGL(f, dim3((unsigned)(cnt * ccount)), dim3(RP_NT), rp_chain_lds((int)P.l), s, a);
+            HIPCHK(hipGetLastError());
+            return MPFFT_OK;
+        }
+        if ((rc = flush_chain())) return rc;
+        return pairop_now(op, off, h, i0, cnt, rho);
+    }
+
+    int pairop_now(int op, long off, long h, long i0, long cnt, u64 rho)
     {
         if (cnt <= 0) return MPFFT_OK;
         PairArgs a;
@@ -912,14 +978,26 @@ struct Exec {
 
     // IFFT_radix2_truncate(_twiddle) (mul_fft.c:1733-1790): outputs [off, off+t) known,
     // inputs >= t zero; root of a length-m block = 2^(w NC NR/m)
+    // public entries: the recursion, then whatever it left in the chain
     int itft(long off, long m, long t)
+    {
+        int rc = itft_r(off, m, t);
+        return rc ? rc : flush_chain();
+    }
+    int itft1(long off, long m, long t)
+    {
+        int rc = itft1_r(off, m, t);
+        return rc ? rc : flush_chain();
+    }
+
+    int itft_r(long off, long m, long t)
     {
         int rc;
         const long h = m / 2;
         const bool top = defer_double && off == 0 && m == P.NR;   // its doubling folds into the scaling
         if (t == m) return ifft_block(off, m);
         if (t <= h) {
-            if ((rc = itft(off, h, t))) return rc;
+            if ((rc = itft_r(off, h, t))) return rc;
             if (top) {
                 dbl_lo = 0;
                 dbl_hi = t;
@@ -933,7 +1011,7 @@ struct Exec {
         fill = {};
         if (rc) return rc;
         if (!filled && (rc = pairop(OP_FILL, off, h, t - h, h - (t - h), rho_blk(m)))) return rc;
-        if ((rc = itft1(off + h, h, t - h))) return rc;
+        if ((rc = itft1_r(off + h, h, t - h))) return rc;
         if ((rc = pairop(OP_IBFLY, off, h, 0, t - h, rho_blk(m)))) return rc;
         if (top) {
             dbl_lo = t - h;
@@ -944,19 +1022,19 @@ struct Exec {
     }
 
     // IFFT_radix2_truncate1(_twiddle) (mul_fft.c:1604-1668): inputs [t, m) known
-    int itft1(long off, long m, long t)
+    int itft1_r(long off, long m, long t)
     {
         int rc;
         const long h = m / 2;
         if (t == m) return ifft_block(off, m);
         if (t <= h) {
             if ((rc = pairop(OP_HALFADD, off, h, t, h - t, 0))) return rc;
-            if ((rc = itft1(off, h, t))) return rc;
+            if ((rc = itft1_r(off, h, t))) return rc;
             return pairop(OP_TWOXMY, off, h, 0, t, 0);
         }
         if ((rc = ifft_block(off, h))) return rc;
         if ((rc = pairop(OP_FIX, off, h, t - h, h - (t - h), rho_blk(m)))) return rc;
-        if ((rc = itft1(off + h, h, t - h))) return rc;
+        if ((rc = itft1_r(off + h, h, t - h))) return rc;
         return pairop(OP_IBFLY, off, h, 0, t - h, rho_blk(m));
     }
 

@@ -40,6 +40,10 @@ inline size_t rp_lds(int l, int logg)
 rp_pair_fn rp_pair_get(int l, int op);
 inline size_t rp_pair_lds(int l) { return (size_t)9 * l + 16; }
 
+// k_rchain<PP, NB>: NB = 1..3 TWOXMY steps and the enclosing IBFLY in one launch (Exec::chain)
+rp_pair_fn rp_chain_get(int l, int nb);
+inline size_t rp_chain_lds(int l) { return (size_t)9 * l + 32; }
+
 // k_rscale<PP>: x <- 2^e x, canonical (the 2^-(depth+1) scaling before the combine)
 typedef void (*rp_scale_fn)(uint64_t *, uint64_t *, int *, unsigned, unsigned, unsigned, unsigned, unsigned);
 rp_scale_fn rp_scale_get(int l);

@@ -722,6 +722,66 @@ __global__ __launch_bounds__(RP_NT) void k_rpair(PairArgs a)
     }, (short *)smem, t);
 }
 
+// ---- the tail of the truncated inverse in one kernel -------------------------------------
+// k_rchain<PP, NB>: the recursion of IFFT_radix2_truncate1 (mul_fft.c:1604-1668) ends with
+// NB steps a = 2a - b on the same rows A_i = off + i (partners at off + hb[j] + i, innermost
+// first), and the enclosing IFFT_radix2_truncate(1) (:1733-1790) then runs its inverse
+// butterfly with A as the bottom rows: t = 2^-e_i A, X, A = X + t, X - t (X_i = xoff + i).
+// One launch reads the NB + 2 coefficients of a column once and writes two (Exec::chain; the
+// separate k_rpair steps read 2 NB + 2 and write NB + 2).
+template <int PP, int NB>
+__global__ __launch_bounds__(RP_NT) void k_rchain(PairArgs a)
+{
+    constexpr int NS = NB + 2;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const RX<PP> X{smem};
+    u32 *SL = (u32 *)(smem + RX<PP>::SB);
+    const int t = threadIdx.x;
+    const int col = (int)(blockIdx.x % a.ncol);
+    const int i = a.i0 + (int)(blockIdx.x / a.ncol);
+    const u32 N = (u32)a.N, N2 = 2 * (u32)a.N;
+    const u32 e = (u32)(((u64)i * a.rho) % N2);
+    if (t < NS) {
+        const long row = t == 0 ? a.off + i : t <= NB ? a.off + a.hb[t - 1] + i : a.xoff + i;
+        SL[t] = (u32)(row * a.NC + col);
+    }
+    __syncthreads();
+    Coef st;
+    st.dig = a.dig;
+    st.cb = a.cb;
+    st.top = a.top;
+    unsigned short *CODE = (unsigned short *)smem;
+    Pr x[NS][PP];
+    rp_stage_codes<NS, PP>(CODE, st, SL, t);
+    rp_load_limbs<NS, NS, PP>(x, st, SL, t);
+    __syncthreads();
+    rp_decode<NS, NS, PP>(x, CODE, t);
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int r = 0; r < PP; ++r) x[0][r] = pr_sub(pr_add(x[0][r], x[0][r]), x[1 + j][r]);
+    const u32 E = e ? N2 - e : 0;   // workgroup-uniform
+    if (E) {
+        rp_pub<PP>(X, 0, x[0], t);
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < PP; ++r) {
+            RP_FENCE();
+            if (E % 128 == 0) {
+                bool ng;
+                const Pr v = rp_get_al<PP>(X, 0, t + RP_NT * r, E, N, ng);
+                x[0][r] = pr_cneg(v, ng);
+            } else {
+                x[0][r] = rp_get_gen<PP>(X, 0, t + RP_NT * r, E, N);
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < PP; ++r) pr_bfly(x[NS - 1][r], x[0][r], x[NS - 1][r], x[0][r], false);
+    __syncthreads();   // HX (rp_store) overlays the exchange slot and the codes
+    rp_store<NS, NS, PP>(x, st, SL, [&](int k) -> bool { return k == 0 || k == NS - 1; }, (short *)smem, t);
+}
+
 // ---- canonicalisation of a slot-form coefficient by all the waves of a workgroup -----------
 // Wave-level: f[64 u0 ...] += sv (sub: -= sv), the carry rippling upward until it dies
 // (almost always in the first limb); returns 1 if it ran off limb l - 1 (the value left

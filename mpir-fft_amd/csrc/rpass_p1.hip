@@ -39,6 +39,12 @@ rp_fn rp_get(int l, int logg, int dir, int mode)
     return nullptr;
 }
 
+rp_pair_fn rp_chain_get_p1(int nb)
+{
+    static const rp_pair_fn tab[4] = {nullptr, k_rchain<1, 1>, k_rchain<1, 2>, k_rchain<1, 3>};
+    return nb >= 1 && nb <= 3 ? tab[nb] : nullptr;
+}
+
 rp_pair_fn rp_pair_get_p1(int op)
 {
     static const rp_pair_fn tab[6] = {k_rpair<1, OP_DOUBLE>, k_rpair<1, OP_HALFADD>, k_rpair<1, OP_FILL>,
@@ -48,6 +54,18 @@ rp_pair_fn rp_pair_get_p1(int op)
 
 rp_pair_fn rp_pair_get_p2(int op);
 rp_pair_fn rp_pair_get_p4(int op);
+rp_pair_fn rp_chain_get_p2(int nb);
+rp_pair_fn rp_chain_get_p4(int nb);
+
+rp_pair_fn rp_chain_get(int l, int nb)
+{
+    switch (l) {
+    case 1024: return rp_chain_get_p1(nb);
+    case 2048: return rp_chain_get_p2(nb);
+    case 4096: return rp_chain_get_p4(nb);
+    }
+    return nullptr;
+}
 
 rp_pair_fn rp_pair_get(int l, int op)
 {

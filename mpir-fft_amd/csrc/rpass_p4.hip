@@ -26,6 +26,12 @@ rp_fn rp_get_p4(int logg, int dir, int mode)
     return tab[dir][mode][logg];
 }
 
+rp_pair_fn rp_chain_get_p4(int nb)
+{
+    static const rp_pair_fn tab[4] = {nullptr, k_rchain<4, 1>, k_rchain<4, 2>, k_rchain<4, 3>};
+    return nb >= 1 && nb <= 3 ? tab[nb] : nullptr;
+}
+
 rp_pair_fn rp_pair_get_p4(int op)
 {
     static const rp_pair_fn tab[6] = {k_rpair<4, OP_DOUBLE>, k_rpair<4, OP_HALFADD>, k_rpair<4, OP_FILL>,
