@@ -1059,10 +1059,15 @@ struct Exec {
         u64 *dig = col.dig[0] + s0 * P.l, *cbp = col.cb[0] + s0 * cb_words((int)P.l);
         int *top = col.top[0] + s0;
         if (P.rpass) {   // register-resident scale + canonicalisation (rkernels.hpp)
-            rp_scale_fn f = rp_scale_get((int)P.l);
+            // threads per coefficient: 256 up to l = 2048 (C3 scale 0.36 -> 0.31 ms: more coefficients
+            // in flight per CU), 512 at l = 4096 (C4 2.61 vs 2.96 ms: the canonical sweep's rows per
+            // wave double); profiles/r03/scale_nt_ab.txt
+            static const int snt_env = [] { const char *e = diag_env("MPFFT_SCALE_NT"); return e ? atoi(e) : 0; }();
+            const int snt = snt_env == 256 || snt_env == 512 ? snt_env : P.l <= 2048 ? 256 : 512;
+            rp_scale_fn f = rp_scale_get((int)P.l, snt);
             if (!f) return MPFFT_EUNSUPPORTED;
             const unsigned lo = (unsigned)((d0 - r0_) * ccount), hi = (unsigned)((d1 - r0_) * ccount);
-            hipLaunchKernelGGL(f, dim3((unsigned)cnt), dim3(RP_NT), rp_scale_lds((int)P.l), s, dig, cbp, top, (unsigned)P.N,
+            hipLaunchKernelGGL(f, dim3((unsigned)cnt), dim3(snt), rp_scale_lds((int)P.l), s, dig, cbp, top, (unsigned)P.N,
                                (unsigned)e, (unsigned)(e + 1), d1 > d0 ? lo : 0u, d1 > d0 ? hi : 0u);
             HIPCHK(hipGetLastError());
             return MPFFT_OK;

@@ -46,5 +46,6 @@ inline size_t rp_chain_lds(int l) { return (size_t)9 * l + 32; }
 
 // k_rscale<PP>: x <- 2^e x, canonical (the 2^-(depth+1) scaling before the combine)
 typedef void (*rp_scale_fn)(uint64_t *, uint64_t *, int *, unsigned, unsigned, unsigned, unsigned, unsigned);
-rp_scale_fn rp_scale_get(int l);
+rp_scale_fn rp_scale_get(int l, int nt = 512);   // nt: threads per workgroup (512 or 256)
 inline size_t rp_scale_lds(int l) { return (size_t)9 * l + (size_t)l + 128; }   // slot + pair overflows + canon scratch
+// threads per k_rscale workgroup (diagnostic A/B: MPFFT_SCALE_NT=256)

@@ -904,11 +904,11 @@ __device__ int rp_canon_par(const BSlot &b, int l, int wave, int lane, int *scr)
 // mpn_normmod_2expp1 :272) by all eight waves, one segment each (rp_canon_par);
 // the canonical residue in [0, 2^N] is stored with zero carry masks and its carry limb.
 // Coefficients [lo, hi) of the launch take exponent e2 instead of e (one launch for all rows).
-template <int PP>
-__global__ __launch_bounds__(RP_NT) void k_rscale(u64 *dig, u64 *cb, int *top, u32 N, u32 e, u32 e2, u32 lo, u32 hi)
+template <int PP, int NT = RP_NT>
+__global__ __launch_bounds__(NT) void k_rscale(u64 *dig, u64 *cb, int *top, u32 N, u32 e, u32 e2, u32 lo, u32 hi)
 {
     if (blockIdx.x >= lo && blockIdx.x < hi) e = e2;   // itft's deferred doubling: those rows by 2^-depth
-    constexpr int l = 1024 * PP, HP = l / 2, cbw = 2 * l / 64;
+    constexpr int l = 1024 * PP, HP = l / 2, cbw = 2 * l / 64, R = rp_r(PP, NT);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const RX<PP> X{smem};
     u32 *SL = (u32 *)(smem + RX<PP>::SB);
@@ -920,46 +920,46 @@ __global__ __launch_bounds__(RP_NT) void k_rscale(u64 *dig, u64 *cb, int *top, u
     st.cb = cb;
     st.top = top;
     unsigned short *CODE = (unsigned short *)smem;
-    Pr x[1][PP];
+    Pr x[1][R];
     rp_stage_codes<1, PP>(CODE, st, SL, t);
-    rp_load_limbs<1, 1, PP>(x, st, SL, t);
+    rp_load_limbs<1, 1, PP, NT>(x, st, SL, t);
     __syncthreads();
-    rp_decode<1, 1, PP>(x, CODE, t);
-    rp_pub<PP>(X, 0, x[0], t);
+    rp_decode<1, 1, PP, NT>(x, CODE, t);
+    rp_pub<PP, NT>(X, 0, x[0], t);
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < PP; ++r) x[0][r] = rp_get_gen<PP>(X, 0, t + RP_NT * r, e, N);
+    for (int r = 0; r < R; ++r) x[0][r] = rp_get_gen<PP>(X, 0, t + NT * r, e, N);
     __syncthreads();
     // k_bpass slot form: f_m, c_m = carry into limb m (the overflow of pair m/2 - 1 for even
     // m, minus the last pair's for m = 0: 2^N == -1), zero for odd m
     const BSlot b = bp_slot(smem, 0, l);
     short *hx = (short *)(smem + bp_slot_bytes(l));   // after the slot: HP pair overflows
 #pragma unroll
-    for (int r = 0; r < PP; ++r) {
-        const int pp = t + RP_NT * r;
+    for (int r = 0; r < R; ++r) {
+        const int pp = t + NT * r;
         *(rp_v4u *)(b.f + 2 * pp) = pr_words(x[0][r]);
         hx[pp] = (short)x[0][r].h;
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < PP; ++r) {
-        const int pp = t + RP_NT * r;
+    for (int r = 0; r < R; ++r) {
+        const int pp = t + NT * r;
         const int hv = hx[pp ? pp - 1 : HP - 1];
         *(short *)(b.c + 2 * pp) = (short)((pp ? hv : -hv) & 0xff);   // c_2pp = hin (|hin| < 128), c_2pp+1 = 0
     }
     __syncthreads();
     {
-        const int tv = rp_canon_par<RP_NT / 64>(b, l, t >> 6, t & 63, (int *)(smem + bp_slot_bytes(l) + (size_t)l));
+        const int tv = rp_canon_par<NT / 64>(b, l, t >> 6, t & 63, (int *)(smem + bp_slot_bytes(l) + (size_t)l));
         if (t == 0) SL[1] = (u32)tv;
     }
     __syncthreads();
     const long sl = blockIdx.x;
     u64 *dst = dig + (size_t)sl * l;
 #pragma unroll
-    for (int r = 0; r < PP; ++r) {
-        const int pp = t + RP_NT * r;
+    for (int r = 0; r < R; ++r) {
+        const int pp = t + NT * r;
         *(rp_v4u *)(dst + 2 * pp) = *(const rp_v4u *)(b.f + 2 * pp);
     }
-    for (int w = t; w < cbw; w += RP_NT) cb[(size_t)sl * cbw + w] = 0;
+    for (int w = t; w < cbw; w += NT) cb[(size_t)sl * cbw + w] = 0;
     if (t == 0) top[sl] = (int)SL[1];
 }

@@ -77,17 +77,20 @@ rp_pair_fn rp_pair_get(int l, int op)
     return nullptr;
 }
 
-void (*rp_scale_get_p1())(u64 *, u64 *, int *, u32, u32, u32, u32, u32) { return k_rscale<1>; }
+void (*rp_scale_get_p1(int nt))(u64 *, u64 *, int *, u32, u32, u32, u32, u32)
+{
+    return nt == 256 ? k_rscale<1, 256> : k_rscale<1>;
+}
 
-void (*rp_scale_get_p2())(u64 *, u64 *, int *, u32, u32, u32, u32, u32);
-void (*rp_scale_get_p4())(u64 *, u64 *, int *, u32, u32, u32, u32, u32);
+void (*rp_scale_get_p2(int nt))(u64 *, u64 *, int *, u32, u32, u32, u32, u32);
+void (*rp_scale_get_p4(int nt))(u64 *, u64 *, int *, u32, u32, u32, u32, u32);
 
-rp_scale_fn rp_scale_get(int l)
+rp_scale_fn rp_scale_get(int l, int nt)
 {
     switch (l) {
-    case 1024: return rp_scale_get_p1();
-    case 2048: return rp_scale_get_p2();
-    case 4096: return rp_scale_get_p4();
+    case 1024: return rp_scale_get_p1(nt);
+    case 2048: return rp_scale_get_p2(nt);
+    case 4096: return rp_scale_get_p4(nt);
     }
     return nullptr;
 }

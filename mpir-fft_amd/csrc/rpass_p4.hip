@@ -39,4 +39,7 @@ rp_pair_fn rp_pair_get_p4(int op)
     return op >= 0 && op < 6 ? tab[op] : nullptr;
 }
 
-void (*rp_scale_get_p4())(u64 *, u64 *, int *, u32, u32, u32, u32, u32) { return k_rscale<4>; }
+void (*rp_scale_get_p4(int nt))(u64 *, u64 *, int *, u32, u32, u32, u32, u32)
+{
+    return nt == 256 ? k_rscale<4, 256> : k_rscale<4>;
+}

@@ -1,0 +1,12 @@
+#!/bin/bash
+# k_rscale with 256- vs 512-thread workgroups (diagnostic build, MPFFT_SCALE_NT): the scale
+# canonicalisation tests and the C3 / C4 benches under each.
+cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out && T=${1:-x} && \
+MPFFT_LIB=diag MPFFT_SCALE_NT=256 timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "scale_canon or bench_configs or c2_c3" > gpurun_out/pytest_$T.log 2>&1 && \
+timeout -k 10 200 python3 -u bench.py --config C3 --steps 10 --no-cpu-baseline --e2e-reps 0 > gpurun_out/bench_c3_$T.log 2>&1 && \
+MPFFT_LIB=diag MPFFT_SCALE_NT=256 timeout -k 10 200 python3 -u bench.py --config C3 --steps 10 --no-cpu-baseline --e2e-reps 0 > gpurun_out/bench_c3b_$T.log 2>&1 && \
+timeout -k 10 300 python3 -u bench.py --config C4 --steps 3 --warmup 1 --no-cpu-baseline --e2e-reps 0 > gpurun_out/bench_c4_$T.log 2>&1 && \
+MPFFT_LIB=diag MPFFT_SCALE_NT=256 timeout -k 10 300 python3 -u bench.py --config C4 --steps 3 --warmup 1 --no-cpu-baseline --e2e-reps 0 > gpurun_out/bench_c4b_$T.log 2>&1
+rc=$?; echo "rc=$rc"; tail -2 gpurun_out/pytest_$T.log
+for c in c3 c3b c4 c4b; do python3 -c "import json; d=json.loads(open('gpurun_out/bench_${c}_$T.log').read().strip().splitlines()[-1]); print('$c', round(d['ms_per_step'],3), d['exact'], {k: round(x,3) for k,x in d['stages_ms'].items()})" 2>/dev/null; done
+exit $rc
