@@ -72,6 +72,7 @@ struct Plan {
     long j1, j2, trunc, Tr, len, total;
     int U, tpb, maxlogg;
     int maxlogg_c;      // column passes (forward and inverse); maxlogg: row passes
+    int maxlogg_i;      // inverse (DIT) k_rpass passes, rows and columns (0: as above)
     bool wave;          // wave-owned coefficient kernels (wkernels.hpp), l <= 512
     int wU;             // their limbs per lane
     bool wfull;         // l == 64 wU
@@ -209,6 +210,11 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
             const char *ec = diag_env("MPFFT_RPLOGG");   // diagnostics: fewer levels per pass (A/B)
             if (ec && atoi(ec) >= 1 && atoi(ec) < rl) rl = atoi(ec);
             p->maxlogg = p->maxlogg_c = rl;
+            int ri = rp_maxlogg_dit((int)p->l);
+            const char *ei = diag_env("MPFFT_RPLOGG_INV");
+            if (ei && atoi(ei) >= 1 && atoi(ei) < ri) ri = atoi(ei);
+            if (ec && rl < ri) ri = rl;
+            p->maxlogg_i = ri;
         }
     }
     p->slots = (size_t)(sqrt2 ? 4 : 2) * p->n;
@@ -335,9 +341,9 @@ struct Exec {
 
     // levels in the next pass when `rem` remain: the fewest passes of <= maxlogg
     // levels, balanced (C1 column inverse: 4 + 3 beats 5 + 2 by ~5 us)
-    int split(int rem, bool col = false) const
+    int split(int rem, bool col = false, bool inv = false) const
     {
-        const int ml = col && P.maxlogg_c ? P.maxlogg_c : P.maxlogg;
+        const int ml = inv && P.maxlogg_i ? P.maxlogg_i : col && P.maxlogg_c ? P.maxlogg_c : P.maxlogg;
         const int np = (rem + ml - 1) / ml;
         return (rem + np - 1) / np;
     }
@@ -407,7 +413,7 @@ struct Exec {
     // split, or some level rotation is not a whole number of limb pairs
     int rpass_mode(const PassArgs &a, int logg, int dir) const
     {
-        if (!P.rpass || logg > rp_maxlogg((int)P.l) || a.canon || a.rho % 128) return -1;
+        if (!P.rpass || logg > (dir ? rp_maxlogg_dit((int)P.l) : rp_maxlogg((int)P.l)) || a.canon || a.rho % 128) return -1;
         if (dir == 0) {
             if (a.scale_e || a.tw_mode == 2) return -1;
             if (a.src[0] || a.src[1]) return a.tw_mode || a.pcarry ? -1 : 2;
@@ -816,7 +822,7 @@ struct Exec {
     {
         int hi = P.lbC;
         while (hi > 0) {
-            int k = split(hi);
+            int k = split(hi, false, true);
             PassArgs a = row_args();
             a.lvl0 = hi - k;
             a.tw_mode = (hi - k == 0) ? 2 : 0;
@@ -834,7 +840,7 @@ struct Exec {
         const int lbM = ilog2(m);
         int hi = lbM;
         while (hi > 0) {
-            int k = split(hi, true);
+            int k = split(hi, true, true);
             PassArgs a = col_args();
             a.lbM = lbM;
             a.lvl0 = hi - k;

@@ -13,7 +13,8 @@ typedef void (*rp_pair_fn)(PairArgs);
 
 // k_rpass at l = 4096 with three levels (G = 8: 256 KiB of coefficients per group) runs
 // 1024 threads, one workgroup per CU: every thread still holds 16 limb pairs (80 VGPRs)
-constexpr int rp_nt(int l, int logg) { return l == 4096 && logg == 3 ? 1024 : RP_NT; }
+// likewise the four-level inverse passes at l = 2048 (16 coefficients, one limb pair each)
+constexpr int rp_nt(int l, int logg) { return (l == 4096 && logg == 3) || (l == 2048 && logg == 4) ? 1024 : RP_NT; }
 // limb pairs per thread and coefficient (thread t owns pairs t + NT r)
 constexpr int rp_r(int PP, int NT) { return 512 * PP / NT; }
 
@@ -27,6 +28,8 @@ rp_fn rp_get(int l, int logg, int dir, int mode);
 // most levels per pass: 32 limbs per thread (G l <= 16384 limbs per 512-thread workgroup,
 // 32768 at l = 4096 with 1024 threads)
 inline int rp_maxlogg(int l) { return l == 1024 ? 3 : l == 2048 ? 3 : l == 4096 ? 3 : 0; }   // l = 1024: G = 16 spills
+// inverse (DIT) passes: four levels at l = 2048 (1024 threads, one workgroup per CU)
+inline int rp_maxlogg_dit(int l) { return l == 2048 ? 4 : rp_maxlogg(l); }
 
 // LDS: NX exchange slots of 9 l bytes (limbs + 16-bit pair overflows) and the exponent
 // table.  <= 73 984 B, so two workgroups fit in 160 KiB (l = 4096, G = 8: 147 600 B, one).
