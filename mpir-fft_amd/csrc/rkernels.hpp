@@ -210,6 +210,54 @@ __device__ __forceinline__ Pr rp_get_gen(const RX<PP> &X, int j, int pp, u32 e, 
     return r;
 }
 
+// pair pp of 2^e y for any e < 2N (the general rotation), from two aligned reads: with
+// e = ea + d (ea whole pairs, d < 128 bits), z = 2^ea y has signed pairs z_q = w_q + h_q 2^128
+// (rp_get_al, signs folded), and 2^d z_q = lo(z_q) + hi(z_q) 2^128 with
+// lo(z_q) = (w_q << d) mod 2^128, hi(z_q) = floor(z_q / 2^(128 - d)), so
+//   pair pp of 2^d z = lo(z_pp) + hi(z_(pp-1)),   pair 0: lo(z_0) - hi(z_(HP-1))  (2^N = -1;
+// the negation after the floor, not before).  Checked against exact arithmetic by a Python
+// model of the same decomposition (k_rpass).
+// d = 32 B + s with B, s workgroup-uniform: word selects resolve at compile time (rp_shift_pair<B>)
+// and every bit shift is one v_alignbit -- about a third of rp_get_gen's 64-bit digit arithmetic.
+__device__ __forceinline__ u32 rp_fun(u32 hi, u32 lo, u32 s) { return s ? __builtin_amdgcn_alignbit(hi, lo, 32 - s) : hi; }
+
+template <int B>
+__device__ __forceinline__ Pr rp_shift_pair(const Pr &a, const Pr &b, u32 s, bool sub)
+{
+    const u32 bs = b.h < 0 ? ~0u : 0u;
+    auto aw = [&](int i) -> u32 { return i >= 0 && i < 4 ? a.w[i] : 0u; };            // i compile-time
+    auto bw = [&](int i) -> u32 { return i < 4 ? b.w[i] : i == 4 ? (u32)b.h : bs; };    // i >= 0 compile-time
+    Pr lo, hi;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        lo.w[k] = rp_fun(aw(k - B), aw(k - B - 1), s);        // bits [32k, 32k + 32) of w_pp << d
+        hi.w[k] = rp_fun(bw(k + 4 - B), bw(k + 3 - B), s);    // bits [32k, ..) of floor(z_(pp-1) / 2^(128 - d))
+    }
+    lo.h = 0;
+    hi.h = (int)rp_fun(bw(8 - B), bw(7 - B), s);              // its signed part above 2^128
+    const u32 m = sub ? ~0u : 0u;
+    return pr_addx(lo, hi, m, (u32)sub);
+}
+
+template <int PP>
+__device__ __forceinline__ Pr rp_get_rot(const RX<PP> &X, int j, int pp, u32 e, u32 N)
+{
+    constexpr int HP = RX<PP>::l / 2;
+    const u32 d = e & 127;
+    bool n0, n1;
+    const Pr a = pr_cneg(rp_get_al<PP>(X, j, pp, e - d, N, n0), n0);
+    if (d == 0) return a;   // workgroup-uniform
+    const Pr b = pr_cneg(rp_get_al<PP>(X, j, pp ? pp - 1 : HP - 1, e - d, N, n1), n1);
+    const u32 s = d & 31;
+    const bool wrap = pp == 0;
+    switch (d >> 5) {       // workgroup-uniform
+    case 0: return rp_shift_pair<0>(a, b, s, wrap);
+    case 1: return rp_shift_pair<1>(a, b, s, wrap);
+    case 2: return rp_shift_pair<2>(a, b, s, wrap);
+    default: return rp_shift_pair<3>(a, b, s, wrap);
+    }
+}
+
 // Exponents in 32 bits: every one is reduced mod 2N < 2^20 (l <= 4096), and a level
 // twiddle (k_pass :212-229) is below N (SGPR pressure: the 64-bit forms spilled).
 __device__ __forceinline__ u32 rp_mod2n(u32 e, u32 N2)
@@ -267,7 +315,7 @@ __device__ __forceinline__ void rp_rot_all(Pr (&x)[G][rp_r(PP, NT)], const RX<PP
 #pragma unroll
             for (int r = 0; r < rp_r(PP, NT); ++r) {
                 RP_FENCE();   // one pair position at a time (VGPRs)
-                x[i0 + q][r] = rp_get_gen<PP>(X, q, t + NT * r, e, N);
+                x[i0 + q][r] = rp_get_rot<PP>(X, q, t + NT * r, e, N);
             }
         }
         __syncthreads();
@@ -677,7 +725,7 @@ __global__ __launch_bounds__(RP_NT) void k_rpair(PairArgs a)
                 const Pr v = rp_get_al<PP>(X, 0, t + RP_NT * r, E, N, ng);
                 y[r] = pr_cneg(v, ng);
             } else {
-                y[r] = rp_get_gen<PP>(X, 0, t + RP_NT * r, E, N);
+                y[r] = rp_get_rot<PP>(X, 0, t + RP_NT * r, E, N);
             }
         }
         __syncthreads();
@@ -772,7 +820,7 @@ __global__ __launch_bounds__(RP_NT) void k_rchain(PairArgs a)
                 const Pr v = rp_get_al<PP>(X, 0, t + RP_NT * r, E, N, ng);
                 x[0][r] = pr_cneg(v, ng);
             } else {
-                x[0][r] = rp_get_gen<PP>(X, 0, t + RP_NT * r, E, N);
+                x[0][r] = rp_get_rot<PP>(X, 0, t + RP_NT * r, E, N);
             }
         }
     }
@@ -928,7 +976,7 @@ __global__ __launch_bounds__(NT) void k_rscale(u64 *dig, u64 *cb, int *top, u32 
     rp_pub<PP, NT>(X, 0, x[0], t);
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < R; ++r) x[0][r] = rp_get_gen<PP>(X, 0, t + NT * r, e, N);
+    for (int r = 0; r < R; ++r) x[0][r] = rp_get_rot<PP>(X, 0, t + NT * r, e, N);
     __syncthreads();
     // k_bpass slot form: f_m, c_m = carry into limb m (the overflow of pair m/2 - 1 for even
     // m, minus the last pair's for m = 0: 2^N == -1), zero for odd m
