@@ -413,6 +413,14 @@ __device__ __forceinline__ void rp_stage_codes(unsigned short *CODE, const Coef 
     }
 }
 
+// bit j of the wave-uniform x -> bit 2j: s_bitreplicate doubles every bit, the mask keeps one
+__device__ __forceinline__ u64 rp_spread32(u32 x)
+{
+    u64 v;
+    asm("s_bitreplicate_b64_b32 %0, %1" : "=s"(v) : "s"(x));
+    return v & 0x5555555555555555ull;
+}
+
 // limbs of the first NS slots (slot i at the uniform index SL[i])
 template <int NS, int NSX, int PP, int NT = RP_NT>
 __device__ __forceinline__ void rp_load_limbs(Pr (&x)[NSX][rp_r(PP, NT)], const Coef &st, const u32 *SL, int t)
@@ -480,15 +488,13 @@ __device__ __forceinline__ void rp_store(const Pr (&x)[NSX][rp_r(PP, NT)], const
             u32 w0 = x[i][r].w[0], w1 = x[i][r].w[1];   // x itself stays intact (k_rpass FILL stores it twice)
             add_small(w0, w1, hin, k0);
             *(rp_v4u *)(dst + 2 * pp) = rp_v4u{w0, w1, x[i][r].w[2], x[i][r].w[3]};
-            // mask words of rows 2 (wv + NW r) (NW = NT / 64 waves; pairs of lanes 0..31) and +1 (lanes 32..63): bit 2j
-            // is pair j's even limb (odd limbs carry nothing).  Lane L fetches the carry of pair
-            // L/2 (resp. 32 + L/2), so one ballot over the even lanes is the word.  (One ballot
-            // per sign spread to the even bits on the scalar unit measured slower: ~60 SALU
-            // instructions per word pair against two lane shuffles.)
-            const int ka = __shfl(k0, lane >> 1), kb = __shfl(k0, 32 + (lane >> 1));
-            const bool ev = !(lane & 1);
-            const u64 pa = __ballot(ev && ka == 1), na = __ballot(ev && ka == -1);
-            const u64 pb = __ballot(ev && kb == 1), nb = __ballot(ev && kb == -1);
+            // mask words of rows 2 (wv + NW r) (NW = NT / 64 waves; pairs of lanes 0..31) and +1
+            // (lanes 32..63): bit 2j is pair j's even limb (odd limbs carry nothing) -- one ballot
+            // per sign, each half spread to the even bits by s_bitreplicate (no lane shuffles; a
+            // shift-and-mask spread on the scalar unit measured slower than the shuffles)
+            const u64 bp = __ballot(k0 == 1), bn = __ballot(k0 == -1);
+            const u64 pa = rp_spread32((u32)bp), na = rp_spread32((u32)bn);
+            const u64 pb = rp_spread32((u32)(bp >> 32)), nb = rp_spread32((u32)(bn >> 32));
             if (lane < 2)
                 *(rp_v2u *)(cbp + 2 * (2 * (wv + (NT / 64) * r) + lane)) = lane ? rp_v2u{pb, nb} : rp_v2u{pa, na};
         }
