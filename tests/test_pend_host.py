@@ -64,3 +64,41 @@ def test_pending_closed_form():
                     for s in range(1 << logg):
                         got = group_formula(rho, lbm, lvl0, logg, pos0, 1 << lobits, done, s, 2 * n)
                         assert got == want[pos0 + s * (1 << lobits)]
+
+
+def test_general_rotation_two_reads():
+    """rp_get_rot (rkernels.hpp): 2^e y mod 2^N + 1 for y in the register pair form (128-bit words
+    w_q plus a small signed overflow h_q at 2^128) from two aligned pair reads: e = ea + d,
+    z = 2^ea y (pairwise, signs folded), pair pp of 2^d z = lo(z_pp) + hi(z_pp-1) with
+    lo = (w << d) mod 2^128, hi = floor(z / 2^(128 - d)), and pair 0 subtracting hi of the top
+    pair (2^N == -1, negated after the floor).  Exact big-integer check of that decomposition."""
+    rng = random.Random(11)
+    for hp in (2, 3, 8, 16):
+        n = 128 * hp
+        p = (1 << n) + 1
+        for _ in range(200):
+            w = [rng.getrandbits(128) for _ in range(hp)]
+            h = [rng.randint(-3, 3) for _ in range(hp)]
+            v = sum((w[q] + h[q] * (1 << 128)) << (128 * q) for q in range(hp)) % p
+            e = rng.randrange(2 * n)
+            d, ea = e & 127, e - (e & 127)
+
+            def pair(pp):   # rp_get_al: pair pp of 2^ea y as a signed value
+                sg = ea >= n
+                src = pp - (((ea - n) if sg else ea) >> 7)
+                wr = src < 0
+                src += hp if wr else 0
+                z = w[src] + h[src] * (1 << 128)
+                return -z if wr != sg else z
+
+            out = []
+            for pp in range(hp):
+                a = pair(pp)
+                if d == 0:
+                    out.append(a)
+                    continue
+                b = pair(pp - 1 if pp else hp - 1)
+                lo = ((a % (1 << 128)) << d) % (1 << 128)
+                hi = b >> (128 - d)
+                out.append(lo + (hi if pp else -hi))
+            assert sum(out[q] << (128 * q) for q in range(hp)) % p == v * pow(2, e, p) % p
