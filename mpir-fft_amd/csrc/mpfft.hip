@@ -450,7 +450,7 @@ struct Exec {
             a.ngroups = 1 << (a.lbM - logg);
             dim3 grid((unsigned)((long)a.nsub * a.ngroups), (unsigned)nops);
             static const bool stamps = diag_env("MPFFT_RP_STAMPS") != nullptr;
-            const unsigned nt = (unsigned)rp_nt((int)P.l, logg);
+            const unsigned nt = (unsigned)rp_nt((int)P.l, logg, dir);
             if (stamps) return bp_stamped(f, grid, nt, lds, a, logg, dir);
             hipLaunchKernelGGL(f, grid, dim3(nt), lds, s, a);
             HIPCHK(hipGetLastError());

@@ -14,7 +14,12 @@ typedef void (*rp_pair_fn)(PairArgs);
 // k_rpass at l = 4096 with three levels (G = 8: 256 KiB of coefficients per group) runs
 // 1024 threads, one workgroup per CU: every thread still holds 16 limb pairs (80 VGPRs)
 // likewise the four-level inverse passes at l = 2048 (16 coefficients, one limb pair each)
-constexpr int rp_nt(int l, int logg) { return (l == 4096 && logg == 3) || (l == 2048 && logg == 4) ? 1024 : RP_NT; }
+// and the three-level inverse passes at l = 2048 (half the limb pairs per thread: their
+// 512-thread form spilled 70-130 B of registers)
+constexpr int rp_nt(int l, int logg, int dir = 0)
+{
+    return (l == 4096 && logg == 3) || (l == 2048 && logg == 4) || (l == 2048 && logg == 3 && dir == 1) ? 1024 : RP_NT;
+}
 // limb pairs per thread and coefficient (thread t owns pairs t + NT r)
 constexpr int rp_r(int PP, int NT) { return 512 * PP / NT; }
 

@@ -511,9 +511,9 @@ __device__ __forceinline__ void rp_store(const Pr (&x)[NSX][rp_r(PP, NT)], const
 // (compile-time, so the register-only level and the LDS level are never both in one kernel:
 // a runtime choice between them spilled)
 template <int LOGG, int PP, int DIR, int MODE>
-__global__ __launch_bounds__(rp_nt(1024 * PP, LOGG), 4) void k_rpass(PassArgs a)
+__global__ __launch_bounds__(rp_nt(1024 * PP, LOGG, DIR), 4) void k_rpass(PassArgs a)
 {
-    constexpr int NT = rp_nt(1024 * PP, LOGG), R = rp_r(PP, NT);
+    constexpr int NT = rp_nt(1024 * PP, LOGG, DIR), R = rp_r(PP, NT);
     constexpr bool GX = DIR == 0 ? MODE == 1 : (MODE & 1) != 0, SPLIT = DIR == 0 && MODE == 2,
                    CIN = DIR == 0 && MODE == 3, HL = DIR == 1 && (MODE & 2) != 0,
                    FILL = DIR == 1 && (MODE & 4) != 0;
