@@ -1210,15 +1210,18 @@ static int s2_launch(const Plan &P, const Exec &X, int op, const u64 *srcA, cons
     a.k0 = k0;
     a.tlo = tlo;
     void (*f)(S2Args) = nullptr;
-    switch (P.U) {
+    // l = 2048: four limbs per thread over 512 threads (k_s2op<2> at 1024 threads spilled 388 B)
+    const int U = P.U == 2 && P.l == 2048 && !diag_env("MPFFT_S2_U2") ? 4 : P.U;
+    const int tpb = (int)(P.l / U) < P.tpb ? (int)(P.l / U) : P.tpb;
+    switch (U) {
     case 1: f = k_s2op<1>; break;
     case 2: f = k_s2op<2>; break;
     case 4: f = k_s2op<4>; break;
     }
     if (!f) return MPFFT_EUNSUPPORTED;
-    const size_t lds = lds_bytes((int)P.l, s2_rb(P.U), 3, P.U, X.nw);
+    const size_t lds = lds_bytes((int)P.l, s2_rb(U), 3, U, tpb / 64);
     allow_lds((const void *)f, lds);
-    hipLaunchKernelGGL(f, dim3((unsigned)cnt, (unsigned)nops), dim3(P.tpb), lds, X.s, a);
+    hipLaunchKernelGGL(f, dim3((unsigned)cnt, (unsigned)nops), dim3(tpb), lds, X.s, a);
     HIPCHK(hipGetLastError());
     return MPFFT_OK;
 }
