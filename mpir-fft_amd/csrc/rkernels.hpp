@@ -502,6 +502,20 @@ __device__ __forceinline__ void rp_store(const Pr (&x)[NSX][rp_r(PP, NT)], const
     }
 }
 
+// every coefficient word materialised in a register at this point, and a scheduling fence: the
+// DIT kernels otherwise interleave the last level's butterflies with what follows (the store or
+// the general rotation) and spill 60-130 B; this boundary removes that
+template <int G, int R>
+__device__ __forceinline__ void rp_pin(Pr (&x)[G][R])
+{
+#pragma unroll
+    for (int i = 0; i < G; ++i)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            asm volatile("" : "+v"(x[i][r].w[0]), "+v"(x[i][r].w[1]), "+v"(x[i][r].w[2]), "+v"(x[i][r].w[3]), "+v"(x[i][r].h));
+    RP_FENCE();
+}
+
 // MODE: DIR 0: 0 plain, 1 MFA twiddle on load, 2 split on load (first column pass),
 //               3 plain with inputs that still owe an earlier pass's pending exponents
 //               (PassArgs::pcarry: the first level rotates its partners through LDS too);
@@ -660,12 +674,14 @@ __global__ __launch_bounds__(rp_nt(1024 * PP, LOGG, DIR), 4) void k_rpass(PassAr
     if (DIR == 0 && !a.pkeep) {   // the pending exponents of the last level (whole pairs): one aligned rotation round
         rp_rot_all_al<G, PP, NX, NT>(x, X, [&](int s) -> u32 { return rp_uniform(EXPT[G + s]); }, N, t);
     }
+    if (DIR == 1) rp_pin<G, R>(x);
     if (DIR == 1 && GX) {   // inverse MFA twiddle and/or fused scaling (bp_post)
         rp_rot_all<G, PP, NX, NT>(x, X, [&](int s) -> u32 { return rp_uniform(EXPT[s]); }, N, t);
     }
     RP_STAMP(5);
 
     // ---- store (reduced form) --------------------------------------------------------
+    if (DIR == 1) rp_pin<G, R>(x);
     rp_store<G, G, PP, NT>(x, st, SLT, [&](int i) -> bool {
         return DIR == 1 || ((g.pos0 + i * g.pstep) & ~(g.pstep - 1)) < a.need;
     }, (short *)smem, t);
