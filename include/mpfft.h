@@ -132,7 +132,10 @@ typedef struct mpfft_shard {
                                  limb floor((p NC + c0) bits1 / 64) on (sharded.py) */
     /* optional third row-layout array (NULL: none).  When set and mpfft_shard_row_fused()
      * says so, the row DIF's last level runs inside the pointwise, whose product lands here
-     * (the caller then treats it as the row array of operand 0). */
+     * (the caller then treats it as the row array of operand 0).  Added in MPFFT_VERSION 2:
+     * callers must zero-initialise the whole struct (memset or `= {0}`), so code written for
+     * the version-1 layout that sets only the older fields passes NULL here; a non-NULL
+     * triple is always taken as a live array. */
     uint64_t *rowc_dig, *rowc_cb;
     int *rowc_top;
 } mpfft_shard;
@@ -158,6 +161,57 @@ size_t mpfft_shard_combine_tmp_bytes(long mcount);
 int mpfft_shard_combine(const mpfft_shard *sh, int phase, uint64_t *d_r, long m0, long mcount, long kbase,
                         const uint64_t *halo, int H, void *d_tmp, size_t tmp_bytes, int cin, int *d_sum,
                         void *stream);
+
+/* ---- multi-GPU from one C process (north_star: "host code stays C") ----------
+ * The same column-sharded multiply as mpir-fft_amd/sharded.py (one process per GPU over
+ * RCCL), driven from one host thread over G devices: every rank's stages on its own device
+ * stream, the three exchanges as peer copies over xGMI (hipMemcpyPeerAsync; peer access
+ * enabled between distinct devices), ordered by events.
+ *
+ * Partition of one multiply over `world` ranks (a power of two dividing NC):
+ *   rows[world + 1]  row positions: rank d owns live rows [rows[d], rows[d+1])
+ *   M[world + 1]     product limbs: rank d writes limbs [M[d], M[d+1])
+ *   info[5]          C (columns per rank), chunk (operand slice limbs per row position),
+ *                    H (halo coefficients), Tr (= trunc / NC), fused (1: the pointwise takes
+ *                    the row DIF's last level, mpfft_shard_row_fused at ccb = C) */
+int mpfft_shard_partition(long n1, long n2, unsigned long depth, unsigned long w, int world,
+                          long *rows, long *M, long *info);
+
+/* One exchange as element copies between the ranks' arrays (column layout: NR*C slots per
+ * operand; row layout: (rows[d+1]-rows[d])*NC slots), fields dig (l u64 per slot), cb
+ * (cb_words u64 per slot), top (one int32 per slot). */
+typedef struct mpfft_copy {
+    int src, dst;              /* ranks */
+    int op;                    /* operand 0 or 1 */
+    int field;                 /* 0 dig, 1 cb, 2 top */
+    int src_layout, dst_layout;    /* 0 column layout, 1 row layout */
+    long src_off, dst_off, count;  /* in elements of the field */
+} mpfft_copy;
+#define MPFFT_XCHG_COL_TO_ROW 1   /* #1 after the forward columns: both operands, every field */
+#define MPFFT_XCHG_ROW_TO_COL 2   /* #2 after the inverse rows: operand 0, every field */
+#define MPFFT_XCHG_COEFFS 3       /* #3 after the inverse columns: operand 0's canonical limbs */
+/* Number of copies written to out (out == NULL: counted only; cap: out's capacity),
+ * or -MPFFT_* on error. */
+long mpfft_shard_exchange_plan(long n1, long n2, unsigned long depth, unsigned long w, int world, int which,
+                               mpfft_copy *out, long cap);
+
+/* r1 = i1 * i2 (host pointers) sharded over ngpus devices: devices[g] is rank g's HIP device
+ * (NULL: 0 .. ngpus-1; a device may repeat -- ranks sharing one GPU, as the tests do).
+ * ngpus must be a power of two dividing NC = 2^floor(depth/2).  Device buffers are cached
+ * per device list (grow-only; mpfft_multi_release frees them).  Not reentrant with itself:
+ * concurrent calls serialise on one lock. */
+int mpfft_mul_multi(uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i2, long n2,
+                    unsigned long depth, unsigned long w, int ngpus, const int *devices);
+int mpfft_multi_release(void);
+
+/* new_mpn_mul / mpfft_mul_ex policy: with ngpus > 1 devices set, products whose coefficients
+ * have >= min_l limbs (0: 1024) and whose NC the device count divides run through
+ * mpfft_mul_multi; everything else on the calling thread's device as before.  ngpus <= 1
+ * turns it off.  The environment variable MPFFT_DEVICES="0,1,...,7" (read at the first
+ * multiply) sets the same policy for callers that cannot call this (an unmodified MPIR). */
+int mpfft_set_devices(int ngpus, const int *devices, long min_l);
+/* Devices the calling thread's last mpfft_mul_ex / new_mpn_mul ran on (1: single device). */
+int mpfft_last_ngpus(void);
 
 /* Stage profiling of the whole-multiply entries (new_mpn_mul, mpfft_mul_ex,
  * mpfft_mul_device): between begin and end, each of the next max_calls multiplies

@@ -45,6 +45,16 @@ class _Shard(ctypes.Structure):
                 ("rowc_dig", ctypes.c_void_p), ("rowc_cb", ctypes.c_void_p), ("rowc_top", ctypes.c_void_p)]
 
 
+class _Copy(ctypes.Structure):
+    """struct mpfft_copy (include/mpfft.h)"""
+    _fields_ = [("src", ctypes.c_int), ("dst", ctypes.c_int), ("op", ctypes.c_int), ("field", ctypes.c_int),
+                ("src_layout", ctypes.c_int), ("dst_layout", ctypes.c_int),
+                ("src_off", ctypes.c_long), ("dst_off", ctypes.c_long), ("count", ctypes.c_long)]
+
+
+XCHG_COL_TO_ROW, XCHG_ROW_TO_COL, XCHG_COEFFS = 1, 2, 3
+
+
 class MpfftError(RuntimeError):
     def __init__(self, code, what):
         super().__init__(f"{what}: {strerror(code)} (code {code})")
@@ -106,6 +116,21 @@ def lib():
         h.mpfft_shard_combine.argtypes = [ctypes.POINTER(_Shard), ctypes.c_int, _vp, _L, _L, _L, _vp, ctypes.c_int,
                                           _vp, ctypes.c_size_t, ctypes.c_int, _vp, _vp]
         h.mpfft_shard_combine.restype = ctypes.c_int
+        _lp = ctypes.POINTER(ctypes.c_long)
+        h.mpfft_shard_partition.argtypes = [_L, _L, _UL, _UL, ctypes.c_int, _lp, _lp, _lp]
+        h.mpfft_shard_partition.restype = ctypes.c_int
+        h.mpfft_shard_exchange_plan.argtypes = [_L, _L, _UL, _UL, ctypes.c_int, ctypes.c_int,
+                                                ctypes.POINTER(_Copy), _L]
+        h.mpfft_shard_exchange_plan.restype = ctypes.c_long
+        h.mpfft_mul_multi.argtypes = [_u64p, _u64p, _L, _u64p, _L, _UL, _UL, ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_int)]
+        h.mpfft_mul_multi.restype = ctypes.c_int
+        h.mpfft_multi_release.argtypes = []
+        h.mpfft_multi_release.restype = ctypes.c_int
+        h.mpfft_set_devices.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), _L]
+        h.mpfft_set_devices.restype = ctypes.c_int
+        h.mpfft_last_ngpus.argtypes = []
+        h.mpfft_last_ngpus.restype = ctypes.c_int
         h.mpfft_choose.argtypes = [_L, _L, ctypes.POINTER(ctypes.c_ulong), ctypes.POINTER(ctypes.c_ulong)]
         h.mpfft_choose.restype = ctypes.c_int
         h.mpfft_mul_auto.argtypes = [_u64p, _u64p, _L, _u64p, _L]
@@ -386,3 +411,52 @@ def shard_combine(desc, phase, d_r, m0, mcount, kbase, halo, H, tmp, cin, d_sum,
                                    _ptr(tmp), tmp.numel(), cin, _ptr(d_sum), _stream(stream))
     if rc:
         raise MpfftError(rc, f"mpfft_shard_combine(phase {phase})")
+
+
+# ---- multi-GPU from one process (mpfft_mul_multi, multi.hip) ------------------------
+
+def shard_partition(n1, n2, depth, w, world):
+    """The C partition of one column-sharded multiply: dict rows, M (lists of world + 1),
+    C, chunk, H, Tr, fused (mpfft_shard_partition)."""
+    rows = (ctypes.c_long * (world + 1))()
+    M = (ctypes.c_long * (world + 1))()
+    info = (ctypes.c_long * 5)()
+    rc = lib().mpfft_shard_partition(n1, n2, depth, w, world, rows, M, info)
+    if rc:
+        raise MpfftError(rc, f"shard_partition(world={world})")
+    return {"rows": list(rows), "M": list(M), "C": info[0], "chunk": info[1], "H": info[2], "Tr": info[3],
+            "fused": bool(info[4])}
+
+
+def shard_exchange_plan(n1, n2, depth, w, world, which):
+    """The copies of exchange `which` (XCHG_*): list of dicts (mpfft_shard_exchange_plan)."""
+    n = lib().mpfft_shard_exchange_plan(n1, n2, depth, w, world, which, None, 0)
+    if n < 0:
+        raise MpfftError(-n, f"shard_exchange_plan(world={world}, which={which})")
+    out = (_Copy * max(n, 1))()
+    n = lib().mpfft_shard_exchange_plan(n1, n2, depth, w, world, which, out, n)
+    if n < 0:
+        raise MpfftError(-n, "shard_exchange_plan")
+    return [{f: getattr(out[i], f) for f, _ in _Copy._fields_} for i in range(n)]
+
+
+def mul_multi(i1, i2, depth, w, devices):
+    """r = i1 * i2 column-sharded over len(devices) ranks (devices may repeat), one process."""
+    i1 = np.ascontiguousarray(i1, dtype=np.uint64)
+    i2 = np.ascontiguousarray(i2, dtype=np.uint64)
+    r = np.zeros(len(i1) + len(i2), dtype=np.uint64)
+    devs = (ctypes.c_int * len(devices))(*devices)
+    rc = lib().mpfft_mul_multi(_p(r), _p(i1), len(i1), _p(i2), len(i2), depth, w, len(devices), devs)
+    if rc:
+        raise MpfftError(rc, f"mul_multi(devices={list(devices)})")
+    return r
+
+
+def set_devices(devices, min_l=0):
+    """new_mpn_mul policy: shard products with >= min_l-limb coefficients over `devices`."""
+    devs = (ctypes.c_int * max(len(devices), 1))(*devices)
+    return lib().mpfft_set_devices(len(devices), devs, min_l)
+
+
+def multi_release():
+    return lib().mpfft_multi_release()

@@ -53,11 +53,12 @@ struct PassArgs {
     unsigned *zp;        // non-null: clear zp[0, zn) (the combine's look-back flags) -- saves a fill launch
     long zn;
     unsigned long long *dbg;   // diagnostics only (MPFFT_BP_STAMPS): per-workgroup s_memtime phase stamps
-    // Pending exponents carried across k_rpass DIF passes (rkernels.hpp, single-GPU run_all only):
+    // Pending exponents carried from one k_rpass DIF pass to the next pass of the same
+    // transform (rkernels.hpp; every Exec, the stage API and the sharded path included: a
+    // transform's last level leaves no pending exponent, so every stage output is exact and
+    // nothing is handed across a stage boundary):
     int pcarry;          // the inputs still owe the DIF pending exponents of levels [lvl0 - pcarry, lvl0)
     int pkeep;           // leave every pending exponent in the output (the next pass applies them)
-    int ccarry;          // first row pass (tw_mode 1): the input owes the column DIF's pending
-                         // exponents of levels [tw_lbR - ccarry, tw_lbR) at its row
     // the truncated inverse's FILL step folded into a block's last DIT pass (k_rpass DIR 1,
     // mode bit 2): positions p >= fill_lo also store 2^(p fill_rho) x_p at position p + fill_off
     int fill_lo, fill_off;

@@ -25,6 +25,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <mutex>
+#include <vector>
 
 #include "kernels.hpp"
 #include "combine.hpp"
@@ -73,6 +74,7 @@ struct Plan {
     int U, tpb, maxlogg;
     int maxlogg_c;      // column passes (forward and inverse); maxlogg: row passes
     int maxlogg_i;      // inverse (DIT) k_rpass passes, rows and columns (0: as above)
+    int bp_lg;          // most levels k_bpass fits in LDS (big): a pass k_rpass declines is capped to it
     bool wave;          // wave-owned coefficient kernels (wkernels.hpp), l <= 512
     int wU;             // their limbs per lane
     bool wfull;         // l == 64 wU
@@ -198,6 +200,7 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
         int lg = 1;
         while (lg < BP_MAXLOGG && bp_lds_need(p->l, 2 << lg) <= BP_LDS_MAX) ++lg;
         p->maxlogg = lg;
+        p->bp_lg = lg;
         // columns: two 74 KB groups per CU beat one 147 KB group at l = 2048 (C3 sweep,
         // profiles/r02/sweep_blogg.txt: columns 5.97 ms vs 6.53 ms; rows 4.71 vs 4.44)
         p->maxlogg_c = lg >= 3 ? lg - 1 : lg;
@@ -291,6 +294,10 @@ static void allow_lds(const void *f, size_t bytes)
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { last_hip_error = e_; return MPFFT_EHIP; } } while (0)
 static thread_local hipError_t last_hip_error = hipSuccess;
+void mpfft_note_hip_error(hipError_t e) { last_hip_error = e; }   // multi.hip's failures
+
+// multi.hip: the device list mpfft_set_devices / MPFFT_DEVICES picks for this product (0: none)
+int mpfft_multi_policy(long n1, long n2, unsigned long depth, unsigned long w, std::vector<int> &devs);
 
 // Where one rank's data lives.  The column layout (slot = pos * ccount + c - c0)
 // feeds the column passes; the row layout (rows r0 .. r0 + rcount of `nblk` column
@@ -317,23 +324,20 @@ struct Exec {
     int in_rows = 0;         // non-zero: inputs live in column rows [0, in_rows) (default: the trunc rows)
     bool defer_double = false;   // itft's top-level doubling is left to scale() (rows [dbl_lo, dbl_hi): 2^-depth)
     bool fuse_row_last = false;  // the row DIF's last level runs inside the pointwise (k_pwss PAIR)
-    // forward k_rpass passes hand their pending exponents on (fwd_columns / fwd_rows).  Every
-    // stage still ends exact: a transform's last level leaves no pending exponent, and the last
-    // row pass (before the pointwise) never hands on -- so the stage API and the sharded path
-    // use it too.
+    // forward k_rpass passes hand their pending exponents on to the next pass of the same
+    // transform (fwd_columns / fwd_rows).  Every stage still ends exact -- a transform's last
+    // level leaves no pending exponent (its pass skips the closing round) -- so the stage API
+    // and the sharded path run the same passes.
     bool carry_pend = !diag_env("MPFFT_NO_CARRY");
-    // which hand-overs: 1 column -> column, 2 last column -> first row (its MFA twiddle rotation
-    // absorbs them; a no-op in practice: after a transform's last level every DIF pending
-    // exponent is 0), 4 row -> row.  A hand-over into a plain pass moves that pass's first level
-    // from registers to an LDS round, about what the skipped closing round costs: measured
-    // (profiles/r03/carry_ab.txt) row -> row pays at l = 2048 and 4096, column -> column only
-    // at l = 4096 (C3 columns 2.02 -> 2.08 ms with it, C4 20.7 -> 19.9 ms).
+    // which hand-overs: 1 column -> column, 4 row -> row.  A hand-over into a plain pass moves
+    // that pass's first level from registers to an LDS round, about what the skipped closing
+    // round costs: measured (profiles/r03/carry_ab.txt) row -> row pays at l = 2048 and 4096,
+    // column -> column only at l = 4096 (C3 columns 2.02 -> 2.08 ms with it, C4 20.7 -> 19.9 ms).
     int carry_mask() const
     {
         static const int m = [] { const char *e = diag_env("MPFFT_CARRY_MASK"); return e ? atoi(e) : -1; }();
-        return m >= 0 ? m : P.l >= 4096 ? 7 : 6;
+        return m >= 0 ? m : P.l >= 4096 ? 5 : 4;
     }
-    int col_carry = 0;           // column levels whose pending exponents the first row pass applies
     struct Fill { long lo = 0, off = 0; u64 rho = 0; bool done = false; } fill;   // itft's FILL, see ifft_block
     long dbl_lo = 0, dbl_hi = 0;
 
@@ -434,6 +438,16 @@ struct Exec {
         static const int rmask = [] { const char *e = diag_env("MPFFT_RPASS_OFF"); return e ? atoi(e) : 0; }();
         if (rm >= 0 && (rmask >> (4 * dir + rm) & 1)) rm = -1;   // diagnostics: bit 4 dir + mode off
         return rm;
+    }
+
+    // levels of a pass whose arguments mk(k) builds: k, unless k_rpass declines that pass and
+    // k_bpass cannot hold 2^k coefficients in LDS (k_rpass takes more levels per pass than
+    // k_bpass fits: three at l = 4096, four inverse at l = 2048) -- then k_bpass's limit
+    template <typename MK>
+    int fit(int k, int dir, MK mk) const
+    {
+        if (!P.big || !P.bp_lg || k <= P.bp_lg || rp_mode(mk(k), k, dir) >= 0) return k;
+        return P.bp_lg;
     }
 
     int pass(PassArgs a, int logg, int dir, int nops)
@@ -610,12 +624,11 @@ struct Exec {
         return a;
     }
 
-    // Pending exponents across forward passes (carry_pend): a
-    // k_rpass DIF pass whose successor is also a k_rpass DIF pass skips its closing rotation
-    // round (the last level's pending exponents, one LDS round trip of all G coefficients) and
-    // leaves them in HBM; the successor folds them into its first level's partner rotations
-    // (PassArgs::pcarry) or, for the first row pass, into its MFA twiddle (ccarry).  The stage
-    // API and the sharded path keep every pass self-contained (their stage outputs are exact).
+    // Pending exponents across forward passes (carry_pend): a k_rpass DIF pass whose successor
+    // in the same transform is also a k_rpass DIF pass skips its closing rotation round (the
+    // last level's pending exponents, one LDS round trip of all G coefficients) and leaves them
+    // in HBM; the successor folds them into its first level's partner rotations
+    // (PassArgs::pcarry).  Nothing crosses a stage: the last pass of a transform owes nothing.
     PassArgs col_pass_args(int lvl) const
     {
         PassArgs a = col_args();
@@ -630,9 +643,7 @@ struct Exec {
     int fwd_columns(const u64 *srcA, long nA, const u64 *srcB, long nB, int nops, int op = -1)
     {
         int lvl = 0, pend0 = 0;   // the data still owe the pending exponents of levels [pend0, lvl)
-        col_carry = 0;
         while (lvl < P.lbR) {
-            int k = split(P.lbR - lvl, true);
             PassArgs a = col_pass_args(lvl);
             if (lvl == 0) {
                 a.src[0] = srcA; a.nsrc[0] = nA;
@@ -644,21 +655,18 @@ struct Exec {
             }
             if (op == 1) a.zp = nullptr;   // the combine flags are cleared by operand 0's pass
             a.pcarry = lvl - pend0;
-            if (carry_pend && rp_mode(a, k, 0) >= 0 && (carry_mask() & (lvl + k < P.lbR ? 1 : 2))) {
-                if (lvl + k < P.lbR) {
-                    const int k2 = split(P.lbR - lvl - k, true);
-                    a.pkeep = rp_mode(col_pass_args(lvl + k), k2, 0) >= 0;
-                } else {
-                    const int L = row_levels();
-                    a.pkeep = L > 0 && rp_mode(row_pass_args(0, split(L), L), split(L), 0) >= 0;
-                }
+            const int k = fit(split(P.lbR - lvl, true), 0, [&](int) { return a; });
+            if (carry_pend && rp_mode(a, k, 0) >= 0 && (carry_mask() & 1) && lvl + k < P.lbR) {
+                const int k2 = split(P.lbR - lvl - k, true);
+                PassArgs n = col_pass_args(lvl + k);
+                n.pcarry = lvl + k - pend0;
+                a.pkeep = rp_mode(n, k2, 0) >= 0;
             }
             int rc = op < 0 ? pass(a, k, 0, nops) : pass(only(a, op), k, 0, 1);
             if (rc) return rc;
             lvl += k;
             if (!a.pkeep) pend0 = lvl;
         }
-        col_carry = P.lbR - pend0;   // consumed by the next fwd_rows
         return MPFFT_OK;
     }
 
@@ -689,20 +697,24 @@ struct Exec {
         int lvl = 0, pend0 = 0;
         const int L = row_levels();
         while (lvl < L) {
-            int k = split(L - lvl);
-            PassArgs a = row_pass_args(lvl, k, L);
-            a.pcarry = lvl - pend0;
-            if (lvl == 0) a.ccarry = col_carry;
+            auto mk = [&](int kk) {
+                PassArgs b = row_pass_args(lvl, kk, L);
+                b.pcarry = lvl - pend0;
+                return b;
+            };
+            const int k = fit(split(L - lvl), 0, mk);
+            PassArgs a = mk(k);
             if (carry_pend && (carry_mask() & 4) && lvl + k < L && rp_mode(a, k, 0) >= 0) {
                 const int k2 = split(L - lvl - k);
-                a.pkeep = rp_mode(row_pass_args(lvl + k, k2, L), k2, 0) >= 0;
+                PassArgs n = row_pass_args(lvl + k, k2, L);
+                n.pcarry = lvl + k - pend0;
+                a.pkeep = rp_mode(n, k2, 0) >= 0;
             }
             int rc = op < 0 ? pass(a, k, 0, nops) : pass(only(a, op), k, 0, 1);
             if (rc) return rc;
             lvl += k;
             if (!a.pkeep) pend0 = lvl;
         }
-        col_carry = 0;
         return MPFFT_OK;
     }
 
@@ -822,10 +834,14 @@ struct Exec {
     {
         int hi = P.lbC;
         while (hi > 0) {
-            int k = split(hi, false, true);
-            PassArgs a = row_args();
-            a.lvl0 = hi - k;
-            a.tw_mode = (hi - k == 0) ? 2 : 0;
+            auto mk = [&](int kk) {
+                PassArgs b = row_args();
+                b.lvl0 = hi - kk;
+                b.tw_mode = (hi - kk == 0) ? 2 : 0;
+                return b;
+            };
+            const int k = fit(split(hi, false, true), 1, mk);
+            PassArgs a = mk(k);
             int rc = pass(a, k, 1, 1);
             if (rc) return rc;
             hi -= k;
@@ -840,18 +856,22 @@ struct Exec {
         const int lbM = ilog2(m);
         int hi = lbM;
         while (hi > 0) {
-            int k = split(hi, true, true);
-            PassArgs a = col_args();
-            a.lbM = lbM;
-            a.lvl0 = hi - k;
-            a.rho = rho_blk(m);
-            a.pos_off = (int)off;
-            a.zero_from = (int)m;
-            a.need = (int)m;
-            if (P.fuse_scale && hi - k == 0 && m == P.NR) {   // the whole column inverse is this block
-                a.scale_e = 2 * P.N - (u64)(P.depth + 1);
-                a.canon = 1;
-            }
+            auto mk = [&](int kk) {
+                PassArgs b = col_args();
+                b.lbM = lbM;
+                b.lvl0 = hi - kk;
+                b.rho = rho_blk(m);
+                b.pos_off = (int)off;
+                b.zero_from = (int)m;
+                b.need = (int)m;
+                if (P.fuse_scale && hi - kk == 0 && m == P.NR) {   // the whole column inverse is this block
+                    b.scale_e = 2 * P.N - (u64)(P.depth + 1);
+                    b.canon = 1;
+                }
+                return b;
+            };
+            const int k = fit(split(hi, true, true), 1, mk);
+            PassArgs a = mk(k);
             if (hi - k == 0 && fill.off) {   // the block's last pass also does the pending FILL step
                 PassArgs f = a;
                 f.fill_lo = (int)fill.lo;
@@ -1651,12 +1671,21 @@ static int mul_host(const Plan &P, uint64_t *r1, const uint64_t *i1, long n1, co
     return MPFFT_OK;
 }
 
+static thread_local int g_last_ngpus = 0;
+int mpfft_last_ngpus(void) { return g_last_ngpus; }
+
 int mpfft_mul_ex(uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i2, long n2, unsigned long depth,
                  unsigned long w)
 {
     Plan P;
     int rc = make_plan(&P, n1, n2, depth, w);
     if (rc) return rc;
+    std::vector<int> devs;
+    if (mpfft_multi_policy(n1, n2, depth, w, devs) > 1) {   // column-sharded over the policy's devices
+        g_last_ngpus = (int)devs.size();
+        return mpfft_mul_multi(r1, i1, n1, i2, n2, depth, w, (int)devs.size(), devs.data());
+    }
+    g_last_ngpus = 1;
     return mul_host(P, r1, i1, n1, i2, n2);
 }
 

@@ -16,9 +16,14 @@ typedef void (*rp_pair_fn)(PairArgs);
 // likewise the four-level inverse passes at l = 2048 (16 coefficients, one limb pair each)
 // and the three-level inverse passes at l = 2048 (half the limb pairs per thread: their
 // 512-thread form spilled 70-130 B of registers)
+#ifdef MPFFT_FWD1K
+#define RP_FWD1K 1
+#else
+#define RP_FWD1K 0
+#endif
 constexpr int rp_nt(int l, int logg, int dir = 0)
 {
-    return (l == 4096 && logg == 3) || (l == 2048 && logg == 4) || (l == 2048 && logg == 3 && dir == 1) ? 1024 : RP_NT;
+    return (l == 4096 && logg == 3) || (l == 2048 && logg == 4) || (l == 2048 && logg == 3 && (dir == 1 || RP_FWD1K)) ? 1024 : RP_NT;
 }
 // limb pairs per thread and coefficient (thread t owns pairs t + NT r)
 constexpr int rp_r(int PP, int NT) { return 512 * PP / NT; }

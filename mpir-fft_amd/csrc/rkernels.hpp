@@ -571,12 +571,7 @@ __global__ __launch_bounds__(rp_nt(1024 * PP, LOGG, DIR), 4) void k_rpass(PassAr
     constexpr int NEXP = 2 * G + (G / 2) * LOGG;
     u32 *EXPT = (u32 *)(smem + NX * RX<PP>::SB);
     u32 *SLT = EXPT + NEXP;
-    // first row pass after columns that kept their pending exponents: the row's column pending
-    // exponent (physical row = column-transform position) joins the MFA twiddle (uniform)
-    const u32 cadd = DIR == 0 && GX && a.ccarry
-                         ? rp_pend_pos((u32)(a.tw_w << a.lbM), a.tw_lbR, a.tw_lbR - a.ccarry, a.tw_lbR, (u32)(a.sub_off + sub), N2)
-                         : 0u;
-    if (t < NEXP) EXPT[t] = rp_exp_entry<LOGG, DIR, GX>(a, g, t, N2, cadd);
+    if (t < NEXP) EXPT[t] = rp_exp_entry<LOGG, DIR, GX>(a, g, t, N2, 0u);
     else if (t < NEXP + G) SLT[t - NEXP] = (u32)slot_lane(t - NEXP);
     __syncthreads();
     const u64 *src = SPLIT ? a.src[op] : nullptr;
@@ -671,7 +666,9 @@ __global__ __launch_bounds__(rp_nt(1024 * PP, LOGG, DIR), 4) void k_rpass(PassAr
         __syncthreads();
         if (li < 3) RP_STAMP(2 + li);
     }
-    if (DIR == 0 && !a.pkeep) {   // the pending exponents of the last level (whole pairs): one aligned rotation round
+    // the pending exponents of the last level (whole pairs): one aligned rotation round -- none
+    // after the transform's last level (rp_pend_pos with hi == lbM is 0 for every position)
+    if (DIR == 0 && !a.pkeep && a.lvl0 + LOGG < a.lbM) {
         rp_rot_all_al<G, PP, NX, NT>(x, X, [&](int s) -> u32 { return rp_uniform(EXPT[G + s]); }, N, t);
     }
     if (DIR == 1) rp_pin<G, R>(x);

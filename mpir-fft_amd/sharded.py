@@ -23,9 +23,10 @@ use all_to_all_single (RCCL over xGMI on GPUs, gloo on CPU for the tests);
 no all-reduce is used.  Each exchange moves one copy of the data: #1 both
 operands, #2 and #3 one.
 """
-import math
-
 import numpy as np
+
+
+XCHG_COL_TO_ROW, XCHG_ROW_TO_COL, XCHG_COEFFS = 1, 2, 3   # include/mpfft.h MPFFT_XCHG_*
 
 
 def cb_words(l):
@@ -33,36 +34,42 @@ def cb_words(l):
 
 
 class ShardPlan:
-    """Partition of one multiply over `world` ranks (pure host arithmetic)."""
+    """Partition of one multiply over `world` ranks: the library's own partition
+    (mpfft_shard_partition, csrc/multi.hip), so this harness and the one-process C driver
+    mpfft_mul_multi shard identically; tests/test_sharded_cpu.py restates it independently."""
 
     def __init__(self, mp, n1, n2, depth, w, world):
         P = mp.plan_info(n1, n2, depth, w)
+        self.mp = mp
         self.n1, self.n2, self.depth, self.w, self.world = n1, n2, depth, w, world
         self.n, self.l, self.NC, self.NR = P["n"], P["l"], P["NC"], P["NR"]
         self.T, self.bits1 = P["trunc"], P["bits1"]
         self.N = self.n * w
         self.len = P["j1"] + P["j2"] - 1
         self.Tr = self.T // self.NC
+        self.total = n1 + n2
+        self.cbw = cb_words(self.l)
         if self.NC % world or world & (world - 1):
             raise ValueError(f"world={world} must be a power of two dividing NC={self.NC}")
-        self.C = self.NC // world                     # columns per rank (= column block of the row layout)
-        self.rows = [(d * self.Tr) // world for d in range(world + 1)]
-        self.total = n1 + n2
-        # output limb ranges: rank d starts at the first limb of coefficient r_d * NC
-        self.M = [0] + [min(self.total, (self.rows[d] * self.NC * self.bits1) // 64) for d in range(1, world)] \
-            + [self.total]
-        # coefficients overlapping limbs >= M_d - 1 that precede rank d's first coefficient
-        self.H = math.ceil((self.N + 128) / self.bits1) + 1
-        self.cbw = cb_words(self.l)
-        for d in range(1, world):
-            if self.rows[d] * self.NC < self.H:
-                raise ValueError("too many ranks for this size (halo spans ranks)")
-            if self.rows[d + 1] - self.rows[d] < 1:
-                raise ValueError("a rank owns no rows")
-
+        try:
+            part = mp.shard_partition(n1, n2, depth, w, world)
+        except mp.MpfftError as e:
+            raise ValueError(f"world={world}: too many ranks for this size ({e})") from None
+        self.C = part["C"]                 # columns per rank (= column block of the row layout)
+        self.rows = part["rows"]           # rank d owns live rows [rows[d], rows[d+1])
+        self.M = part["M"]                 # rank d writes product limbs [M[d], M[d+1])
+        self.H = part["H"]                 # halo: coefficients before a rank's first one that reach its limbs
         # operand column slices (fused split reads them through SrcSlice, coeff.hpp): for
-        # each live position p < Tr, limbs from floor((p NC + c0) bits1 / 64) on
-        self.chunk = (self.C * self.bits1 + 63) // 64 + 2
+        # each live position p < Tr, `chunk` limbs from floor((p NC + c0) bits1 / 64) on
+        self.chunk = part["chunk"]
+        self._xplans = {}
+
+    def exchange_plan(self, which):
+        """the copies of exchange `which` (mp.XCHG_*), from the library (mpfft_shard_exchange_plan)"""
+        if which not in self._xplans:
+            self._xplans[which] = self.mp.shard_exchange_plan(self.n1, self.n2, self.depth, self.w, self.world,
+                                                              which)
+        return self._xplans[which]
 
     def slice_start(self, p, d):
         return ((p * self.NC + d * self.C) * self.bits1) // 64
@@ -105,9 +112,16 @@ class ShardedMul:
         else:
             self.row = [backend.alloc_coeffs(p.row_slots(rank)) for _ in range(2)]
         # the row DIF's last level fused into the pointwise, as on one GPU: the product lands in
-        # a third row array, which then serves as operand 0's row array (swapped after the stage)
+        # a third row array, which then serves as operand 0's row array (swapped after the stage).
+        # At world 1 that array is a view of a third column-layout array, swapped together with
+        # col[0], so the row arrays stay views of the column arrays on every run.
         self.fused = bool(getattr(backend, "row_fused", lambda: False)())
-        self.rowc = backend.alloc_coeffs(p.row_slots(rank)) if self.fused else None
+        self.colc = None
+        if self.fused and p.world == 1:
+            self.colc = backend.alloc_coeffs(p.col_slots())
+            self.rowc = {f: self.colc[f][: p.row_slots(rank) * backend.width(f, p)] for f in self.colc}
+        else:
+            self.rowc = backend.alloc_coeffs(p.row_slots(rank)) if self.fused else None
 
     def shard_desc(self):
         p, d = self.p, self.rank
@@ -115,31 +129,34 @@ class ShardedMul:
                     r0=p.rows[d], rcount=p.rcount(d), ccb=p.C, col=self.col, row=self.row,
                     src_chunk=p.chunk if self.sliced else 0, rowc=self.rowc)
 
-    # all-to-all #1 / #3: column layout rows [r_d, r_{d+1}) -> rank d's row layout block;
-    # every field (and operand) of one exchange goes in one batch of point-to-point ops
-    def _col_to_row(self, ks, fields):
-        p, me = self.p, self.rank
-        plan = []
-        for k in ks:
-            for f in fields:
-                wd = self.be.width(f, p)
-                send = [self.col[k][f][p.rows[d] * p.C * wd: p.rows[d + 1] * p.C * wd] for d in range(p.world)]
-                blk = p.rcount(me) * p.C * wd
-                recv = [self.row[k][f][s * blk: (s + 1) * blk] for s in range(p.world)]
-                plan.append((send, recv))
-        self.comm.exchange(plan)
+    # one exchange from the library's copy plan (the same copies mpfft_mul_multi issues as
+    # peer DMA): #1 column layout rows [r_d, r_{d+1}) -> rank d's row layout block (both
+    # operands), #2 back (the product), #3 the canonical limbs again.  Every (operand, field)
+    # is one (send views by peer, recv views by peer) entry; all go in one batch of
+    # point-to-point ops
+    _FIELDS = ("dig", "cb", "top")
 
-    # all-to-all #2: row layout block s -> rank s's column layout rows [r_d, r_{d+1})
-    def _row_to_col(self, ks, fields):
+    def _exchange(self, which):
         p, me = self.p, self.rank
+        W = p.world
+
+        def arr(layout, k):
+            return self.row[k] if layout else self.col[k]
+        groups = {}
+        for c in p.exchange_plan(which):
+            if me not in (c["src"], c["dst"]):
+                continue
+            f = self._FIELDS[c["field"]]
+            send, recv = groups.setdefault((c["op"], c["field"]), ([None] * W, [None] * W))
+            if c["src"] == me:
+                send[c["dst"]] = arr(c["src_layout"], c["op"])[f][c["src_off"]: c["src_off"] + c["count"]]
+            if c["dst"] == me:
+                recv[c["src"]] = arr(c["dst_layout"], c["op"])[f][c["dst_off"]: c["dst_off"] + c["count"]]
         plan = []
-        for k in ks:
-            for f in fields:
-                wd = self.be.width(f, p)
-                blk = p.rcount(me) * p.C * wd
-                send = [self.row[k][f][s * blk: (s + 1) * blk] for s in range(p.world)]
-                recv = [self.col[k][f][p.rows[d] * p.C * wd: p.rows[d + 1] * p.C * wd] for d in range(p.world)]
-                plan.append((send, recv))
+        for (op, fi) in sorted(groups):
+            send, recv = groups[(op, fi)]
+            empty = self.col[op][self._FIELDS[fi]][:0]
+            plan.append(([v if v is not None else empty for v in send], [v if v is not None else empty for v in recv]))
         self.comm.exchange(plan)
 
     def run(self, i1, i2, mark=None):
@@ -150,7 +167,7 @@ class ShardedMul:
         mark = mark or (lambda name: None)
         be.stage("fwd_columns", sh, i1, i2)
         mark("fwd_columns")
-        self._col_to_row((0, 1), ("dig", "cb", "top"))
+        self._exchange(XCHG_COL_TO_ROW)
         mark("exchange1")
         be.stage("fwd_rows", sh, i1, i2)
         mark("fwd_rows")
@@ -158,14 +175,16 @@ class ShardedMul:
         mark("pointwise")
         if self.fused:   # the product is in rowc: it becomes operand 0's row array
             self.row[0], self.rowc = self.rowc, self.row[0]
-            sh["rowc"] = self.rowc
+            if self.colc is not None:   # world 1: and its column array operand 0's
+                self.col[0], self.colc = self.colc, self.col[0]
+            sh = self.shard_desc()
         be.stage("inv_rows", sh, i1, i2)
         mark("inv_rows")
-        self._row_to_col((0,), ("dig", "cb", "top"))
+        self._exchange(XCHG_ROW_TO_COL)
         mark("exchange2")
         be.stage("inv_columns", sh, i1, i2)
         mark("inv_columns")
-        self._col_to_row((0,), ("dig",))                   # canonical coefficients: limbs only
+        self._exchange(XCHG_COEFFS)                        # canonical coefficients: limbs only
         # halo: the last H coefficients of every rank's range, all-gathered
         halo_all = self.comm.all_gather(be.tail_coeffs(sh, p.H))
         mark("exchange3")
@@ -381,9 +400,25 @@ def bench(args, cfg_name, cfg, rank, world, dev):
     comp = {k: v for k, v in phase_ms.items() if not k.startswith("exchange")}
     dname = max(comp, key=comp.get)
     dbytes = _phase_bytes(P, dname, nl, nl, world)
+    # HBM traffic of the dominant phase's kernel from the committed one-GPU counter pass of the
+    # same product (profiles/pmc_<cfg>.json, rocprofv3 --pmc, gfx950-corrected): a rank's
+    # launch covers 1/world of the slots of the one-GPU launch
+    traffic, tsrc = None, None
+    kern = {"pointwise": "k_pwss"}.get(dname)
+    if kern:
+        try:
+            pmc = json.load(open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                              "profiles", f"pmc_{cfg_name}.json")))
+            for name, rec in pmc.get("kernels", {}).items():
+                if kern in name and rec.get("hbm_bytes_per_launch"):
+                    traffic = rec["hbm_bytes_per_launch"] / world
+                    tsrc = f"profiles/pmc_{cfg_name}.json ({name.split('(')[0]}, one-GPU launch) / world"
+                    break
+        except (OSError, ValueError):
+            pass
     roof = {"bound": "hbm", "achieved": dbytes / (comp[dname] * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
-            "frac": dbytes / (comp[dname] * 1e-3) / 8.0e12, "traffic": None, "stage": dname,
-            "avg_ms": comp[dname], "alg_bytes_per_launch": dbytes,
+            "frac": dbytes / (comp[dname] * 1e-3) / 8.0e12, "traffic": traffic, "traffic_source": tsrc,
+            "stage": dname, "avg_ms": comp[dname], "alg_bytes_per_launch": dbytes,
             "note": "the slowest rank's dominant phase (all of its launches) vs one GPU's HBM peak; "
                     "algorithmic bytes = the phase's whole-multiply bytes / world"}
 
@@ -442,6 +477,9 @@ def bench(args, cfg_name, cfg, rank, world, dev):
             "pipeline": {"b_alg_bytes": balg,
                          "hbm_frac_b_alg": balg / (el / args.steps) / (world * 8.0e12),
                          "note": "whole multiply vs the aggregate HBM roofline of the ranks (SURVEY 8d)"},
+            "cpu_baseline": {"value": None, "unit": "limbs/s", "kind": "port",
+                             "note": "timed on the N = 1 line only (rank 0, bounded sample: the bench contract); "
+                                     "see BENCH_rNN.json cpu_baseline"},
             "e2e_host": {"ms": e2e_ms, "limbs_per_s": 2 * nl / (e2e_ms * 1e-3),
                          "note": "per rank: its operand column slices H2D, the multiply, its product limbs D2H "
                                  "(host slicing excluded); max over ranks"},

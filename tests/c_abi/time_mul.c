@@ -13,7 +13,12 @@
  * usage: time_mul [depth w limbs iters]     -> prints "ok <ms per call>" or "MISMATCH"
  *        time_mul --mul6 depth w limbs iters -> the same through new_mpn_mul6 (the sqrt2
  *                                              front end, mul_fft.c:3573; test_mul4 :5559)
+ *        time_mul --devices 0,1,2,3 depth w limbs iters
+ *                                           -> mpfft_mul_multi: the product column-sharded over
+ *                                              those HIP devices from this one process
  *        time_mul --bad                     -> invalid parameters: new_mpn_mul must abort
+ * With MPFFT_DEVICES=0,1,...,7 in the environment the plain new_mpn_mul calls shard too (the
+ * library's device policy) -- the caller stays unmodified.
  * Built by __graft_entry__.build() (gcc, -lmpfft -lgmp); run by tests/test_c_abi.py.
  */
 #include <gmp.h>
@@ -29,6 +34,20 @@ static double now_ms(void)
     struct timespec ts;
     clock_gettime(CLOCK_MONOTONIC, &ts);
     return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
+static int ndevs;
+static int devs[64];
+
+/* new_mpn_mul's signature over mpfft_mul_multi with the --devices list */
+static void mul_multi(mp_limb_t *r1, mp_limb_t *i1, mp_size_t n1, mp_limb_t *i2, mp_size_t n2, mp_bitcnt_t depth,
+                      mp_bitcnt_t w)
+{
+    int rc = mpfft_mul_multi(r1, i1, n1, i2, n2, depth, w, ndevs, devs);
+    if (rc) {
+        fprintf(stderr, "mpfft_mul_multi: %s\n", mpfft_strerror(rc));
+        exit(2);
+    }
 }
 
 static void random_limbs(mp_limb_t *dst, mp_size_t n, gmp_randstate_t st)
@@ -55,8 +74,16 @@ int main(int argc, char **argv)
         argv++;
         argc--;
     }
+    if (argc > 2 && !strcmp(argv[1], "--devices")) {
+        for (char *q = argv[2]; *q && ndevs < 64;) {
+            devs[ndevs++] = (int)strtol(q, &q, 10);
+            if (*q == ',') q++;
+        }
+        argv += 2;
+        argc -= 2;
+    }
     void (*mul)(mp_limb_t *, mp_limb_t *, mp_size_t, mp_limb_t *, mp_size_t, mp_bitcnt_t, mp_bitcnt_t) =
-        six ? new_mpn_mul6 : new_mpn_mul;
+        six ? new_mpn_mul6 : ndevs ? mul_multi : new_mpn_mul;
     mp_bitcnt_t depth = argc > 4 ? strtoul(argv[1], 0, 0) : 10;
     mp_bitcnt_t w = argc > 4 ? strtoul(argv[2], 0, 0) : 3;
     mp_size_t n = argc > 4 ? strtol(argv[3], 0, 0) : 24000;
@@ -79,8 +106,9 @@ int main(int argc, char **argv)
         printf("MISMATCH depth=%lu w=%lu n=%ld\n", (unsigned long)depth, (unsigned long)w, (long)n);
         return 1;
     }
-    printf("ok %.3f ms per %s (depth=%lu w=%lu n1=n2=%ld, host pointers, H2D+D2H included)\n", per,
-           six ? "new_mpn_mul6" : "new_mpn_mul", (unsigned long)depth, (unsigned long)w, (long)n);
+    printf("ok %.3f ms per %s (depth=%lu w=%lu n1=n2=%ld, host pointers, H2D+D2H included; devices=%d)\n", per,
+           six ? "new_mpn_mul6" : ndevs ? "mpfft_mul_multi" : "new_mpn_mul", (unsigned long)depth, (unsigned long)w,
+           (long)n, ndevs ? ndevs : six ? 1 : mpfft_last_ngpus());
     free(i1);
     gmp_randclear(state);
     return 0;

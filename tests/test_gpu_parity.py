@@ -274,6 +274,46 @@ def test_nested_pointwise_full_products(mp, oracle):
             os.environ["MPFFT_POINTWISE"] = old
 
 
+@pytest.mark.parametrize("depth,w,nl", [(13, 32, 9800000), (11, 128, 2600000), (7, 2048, 150000)])
+def test_fill_fold_l4096_case_b(mp, oracle, depth, w, nl):
+    """The truncated inverse's FILL step folded into the last DIT pass of a block IFFT
+    (k_rpass DIR 1, mode bit 2: a second, rotated store of the same registers) at l = 4096,
+    truncation case b (T > n), with C4's proportions: the top-level block of NR/2 rows runs
+    two or three DIT passes and FILL covers rows [t - h, h).  Guards against the failure that
+    only the full-size C4 digest caught mid round 3 (gpurun_out/pytest_fill1.log: C4 digest
+    a775e4... instead of 36ca70...): a FILL store built from registers the first store had
+    already changed.  Checked against a mutant build with that defect (scripts/mutant_fill.sh:
+    rp_store adding the pair-overflow carry into the registers in place): this test fails on
+    it and passes on the shipped library (profiles/r04/mutant_fill.log)."""
+    P = mp.plan_info(nl, nl, depth, w)
+    assert P["l"] == 4096 and 2 * P["n"] >= P["trunc"] > P["n"], P   # case b
+    assert "k_rpass" in mp.stage_kernels(nl, nl, depth, w)["inv_columns"]
+    a = mp.fill_random(nl, 0x7007 + depth)
+    b = mp.fill_random(nl - 3, 0x8008 + w)
+    assert (mp.mul(a, b, depth, w) == oracle.gmp_mul(a, b)).all()
+
+
+@pytest.mark.parametrize("kind", ["mfma", "mfma1", "valu"])
+def test_l4096_products_every_pointwise_kind(mp, oracle, kind):
+    """Whole products at l = 4096 with every MPFFT_POINTWISE family.  Those kinds need the
+    canonical store in the last forward row pass, which k_rpass declines, so that pass falls
+    back to k_bpass -- which fits only two levels in LDS at l = 4096.  With lbC = 6 (depth 13)
+    the row split is 3 + 3: before the cap (Exec::fit) the last pass asked for k_bpass<3> and
+    the launch failed.  depth 17 (C4's shape, 3 + 3 + 2) beside it."""
+    old = os.environ.get("MPFFT_POINTWISE")
+    os.environ["MPFFT_POINTWISE"] = kind
+    try:
+        for depth, w, n1, n2 in ((13, 32, 1000000, 999983), (17, 2, 1500000, 1400000)):
+            a = mp.fill_random(n1, 0x5005 + depth)
+            b = mp.fill_random(n2, 0x6006 + w)
+            assert (mp.mul(a, b, depth, w) == oracle.gmp_mul(a, b)).all(), (kind, depth, w)
+    finally:
+        if old is None:
+            os.environ.pop("MPFFT_POINTWISE", None)
+        else:
+            os.environ["MPFFT_POINTWISE"] = old
+
+
 def test_mul_auto_exact_across_sizes(mp, oracle):
     """mpn_mul-style entry with the chooser's (depth, w): exact products from 1e3- to
     1e9-bit operands (balanced and unbalanced) against GMP mpn_mul."""

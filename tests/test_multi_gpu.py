@@ -1,0 +1,74 @@
+"""GPU tests of the one-process multi-GPU entry mpfft_mul_multi (csrc/multi.hip) and the
+new_mpn_mul device policy (mpfft_set_devices).  On the one-GPU box every rank is placed on
+device 0: the ranks' stages, the three exchanges (same-device copies instead of xGMI peer
+DMA -- the copy plan, offsets and event ordering are the same), the halo and the cross-rank
+carry scan run exactly as on eight GPUs.  C4 (BASELINE configs[4], 10^10 bits) at world 8
+is checked against its committed GMP digest."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+@pytest.mark.parametrize("depth,w,n1,n2", [(13, 32, 1000000, 999000), (15, 4, 2000000, 1900000),
+                                          (11, 8, 261952, 261952), (10, 1, 2000, 1800)])
+def test_mul_multi_one_device(mp, oracle, world, depth, w, n1, n2):
+    """l = 4096 (8 columns per rank at world 8), l = 2048 (the C2/C3 size, fused row level),
+    C1's shape (l = 256) and a small l = 16 case, every world size, against GMP; the second
+    call reuses the cached buffers."""
+    P = mp.plan_info(n1, n2, depth, w)
+    if P["NC"] % world:
+        pytest.skip("world does not divide NC")
+    a = mp.fill_random(n1, 0x11 + depth + world)
+    b = mp.fill_random(n2, 0x22 + w)
+    want = oracle.gmp_mul(a, b)
+    for _ in range(2):
+        assert (mp.mul_multi(a, b, depth, w, [0] * world) == want).all()
+
+
+def test_mul_multi_c4_world8_digest(mp):
+    """C4 split 8 ways exactly as on an 8-GPU node (32 columns, 74-75 live rows per rank,
+    seven-peer exchanges, halo, carry scan) with all ranks on device 0, against the GMP digest."""
+    with open(os.path.join(HERE, "golden", "products.json")) as f:
+        case = {c["name"]: c for c in json.load(f)}["C4"]
+    n1, n2, depth, w = case["n1"], case["n2"], case["depth"], case["w"]
+    part = mp.shard_partition(n1, n2, depth, w, 8)
+    assert part["C"] == 32 and all(part["rows"][d + 1] - part["rows"][d] in (74, 75) for d in range(8))
+    a = mp.fill_random(n1, int(case["seed1"], 16))
+    b = mp.fill_random(n2, int(case["seed2"], 16))
+    r = mp.mul_multi(a, b, depth, w, [0] * 8)
+    del a, b
+    assert hashlib.sha256(r.tobytes()).hexdigest() == case["sha256"]
+    mp.multi_release()
+
+
+def test_new_mpn_mul_device_policy(mp, oracle):
+    """mpfft_set_devices: new_mpn_mul shards products with coefficients of >= min_l limbs over
+    the listed devices (here four ranks on device 0) and runs smaller ones on one device;
+    both exact.  Turned off again afterwards."""
+    try:
+        mp.set_devices([0, 0, 0, 0], min_l=1024)
+        for depth, w, n1, n2 in ((13, 32, 800000, 700000), (9, 2, 120, 97)):
+            a = mp.fill_random(n1, 0x33 + depth)
+            b = mp.fill_random(n2, 0x44 + depth)
+            assert (mp.mul(a, b, depth, w) == oracle.gmp_mul(a, b)).all()
+            assert mp.lib().mpfft_last_ngpus() == (4 if depth == 13 else 1)
+    finally:
+        mp.set_devices([])
+        mp.multi_release()
+
+
+def test_mul_multi_rejects_bad_worlds(mp):
+    a = mp.fill_random(1000, 1)
+    with pytest.raises(mp.MpfftError):
+        mp.mul_multi(a, a, 10, 1, [0, 0, 0])          # not a power of two
+    with pytest.raises(mp.MpfftError):
+        mp.mul_multi(a, a, 10, 1, [0] * 64)           # more ranks than columns
+    with pytest.raises(mp.MpfftError):
+        mp.mul_multi(a, a, 10, 1, [0, 99])            # no such device

@@ -24,7 +24,9 @@ def _exact(a, b, limbs):
                                           (15, 4, 2000000, 1900000), (13, 32, 1000000, 1000000)])
 def test_sharded_world1(mp, oracle, depth, w, n1, n2):
     """World 1 through the sharded code path (column slices, local exchanges) at l = 32 ... 4096:
-    (15, 4) is a C2/C3-shaped l = 2048 case, (13, 32) an l = 4096 case with 8 row levels."""
+    (15, 4) is a C2/C3-shaped l = 2048 case, (13, 32) an l = 4096 case with 8 row levels.
+    Two runs of the same job: the fused-pointwise array swap must leave the row arrays views
+    of the column arrays, and the second product exact too."""
     import torch
     from mpir_fft_amd.sharded import ShardPlan, ShardedMul, GpuBackend, _SoloComm
     dev = torch.device("cuda:0")
@@ -33,10 +35,15 @@ def test_sharded_world1(mp, oracle, depth, w, n1, n2):
     b = mp.fill_random(n2, 6 + w)
     job = ShardedMul(plan, 0, GpuBackend(mp, plan, dev), _SoloComm())
     sa, sb = plan.slice_operand(a, 0), plan.slice_operand(b, 0)
-    m0, limbs = job.run(torch.from_numpy(sa.view(np.int64)).to(dev), torch.from_numpy(sb.view(np.int64)).to(dev))
-    torch.cuda.synchronize()
-    got = limbs.cpu().numpy().view(np.uint64)
-    assert m0 == 0 and (got == oracle.gmp_mul(a, b)).all()
+    da, db = torch.from_numpy(sa.view(np.int64)).to(dev), torch.from_numpy(sb.view(np.int64)).to(dev)
+    want = oracle.gmp_mul(a, b)
+    for run in range(2):
+        m0, limbs = job.run(da, db)
+        torch.cuda.synchronize()
+        got = limbs.cpu().numpy().view(np.uint64)
+        assert m0 == 0 and (got == want).all(), run
+        for k in range(2):   # world 1: every row array is a view of its column array
+            assert job.row[k]["dig"].data_ptr() == job.col[k]["dig"].data_ptr()
 
 
 def test_sharded_world1_c4_digest(mp):
@@ -59,11 +66,13 @@ def test_sharded_world1_c4_digest(mp):
     sb = torch.from_numpy(plan.slice_operand(b, 0).view(np.int64)).to(dev)
     del b
     job = ShardedMul(plan, 0, GpuBackend(mp, plan, dev), _SoloComm())
-    m0, limbs = job.run(sa, sb)
-    torch.cuda.synchronize()
-    got = limbs.cpu().numpy().view(np.uint64)
-    assert m0 == 0 and len(got) == 2 * nl
-    assert hashlib.sha256(got.tobytes()).hexdigest() == want["sha256"]
+    for run in range(2):   # the second run on swapped (still aliased) arrays
+        m0, limbs = job.run(sa, sb)
+        torch.cuda.synchronize()
+        got = limbs.cpu().numpy().view(np.uint64)
+        assert m0 == 0 and len(got) == 2 * nl
+        assert hashlib.sha256(got.tobytes()).hexdigest() == want["sha256"], run
+        del got
     del job, sa, sb, limbs
     torch.cuda.empty_cache()
 
@@ -114,12 +123,15 @@ def _worker(rank, world, port, depth, w, n1, n2, q):
         dist.destroy_process_group()
 
 
-# two ranks on one GPU, exchanges host-staged through gloo: C1's shape (l = 256), a small
+# ranks sharing one GPU, exchanges host-staged through gloo: C1's shape (l = 256), a small
 # unbalanced case, a depth-15 w-4 case (l = 2048, the C2/C3 coefficient size) and a depth-13
-# w-32 case (l = 4096, the C4 coefficient size, 8 row levels)
+# w-32 case (l = 4096, the C4 coefficient size, 8 row levels) at 2 ranks; the l = 4096 case
+# at 4 and 8 ranks too (C4's world: 8 columns and 2 live rows per rank, seven-peer batches)
 @pytest.mark.parametrize("world,depth,w,n1,n2", [(2, 11, 8, 261952, 261952), (2, 9, 2, 2000, 1500),
-                                                 (2, 15, 4, 2000000, 2000000), (2, 13, 32, 1000000, 1000000)])
-def test_sharded_two_ranks_one_gpu(world, depth, w, n1, n2):
+                                                 (2, 15, 4, 2000000, 2000000), (2, 13, 32, 1000000, 1000000),
+                                                 (4, 13, 32, 1000000, 1000000), (8, 13, 32, 1000000, 1000000),
+                                                 (8, 15, 4, 2000000, 1900000)])
+def test_sharded_ranks_one_gpu(world, depth, w, n1, n2):
     import torch.multiprocessing as tmp
     ctx = tmp.get_context("spawn")
     q = ctx.Queue()
