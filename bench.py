@@ -305,7 +305,7 @@ def main():
         from importlib import import_module
         sh = import_module("mpir_fft_amd.sharded")
         twin = None
-        if rank == 0 and not args.no_twin and not share:   # the same product on one GPU, same run
+        if rank == 0 and not args.no_twin:   # the same product on one GPU, same run
             twin = single_gpu_line(mp, dev, cfg, 3, 1, check=not args.no_check)
         if world > 1:
             dist.barrier()
