@@ -383,28 +383,49 @@ __device__ __forceinline__ void rp_rot_all_al(Pr (&x)[G][rp_r(PP, NT)], const RX
 // Carry masks -> one 16-bit code per limb pair in LDS (low byte: carry out of limb 2pp,
 // high byte: carry out of limb 2pp+1, plus the carry limb for the last pair); one thread
 // per (slot, 64-limb row) of the first NS slots, slot i's index at SL[i] (LDS).
+// Staged in two halves, so a kernel can issue its limb loads between them: the
+// mask (and carry-limb) loads go out first, the limb loads behind them, and the code
+// computation then waits only for the masks (in-order vmcnt) while the limbs are in flight.
+// (staging the codes before the limb loads serialised two HBM round trips: the limb loads'
+// slot indices come from LDS, read after the code stores, which wait for the masks.)
+struct RpCodes {
+    rp_v2u pn;
+    int tv;
+};
+
 template <int NS, int PP>
-__device__ __forceinline__ void rp_stage_codes(unsigned short *CODE, const Coef &st, const u32 *SL, int t)
+__device__ __forceinline__ RpCodes rp_codes_load(const Coef &st, const u32 *SL, int t)
 {
-    constexpr int l = 1024 * PP, HP = l / 2, cbw = 2 * l / 64, rows = l / 64;
-    if (t >= NS * rows) return;
+    constexpr int l = 1024 * PP, cbw = 2 * l / 64, rows = l / 64;
+    RpCodes c{rp_v2u{0, 0}, 0};
+    if (t >= NS * rows) return c;
     const int i = t / rows, W = t % rows;
     const long sl = (long)SL[i];
-    const rp_v2u pn = *(const rp_v2u *)(st.cb + (size_t)sl * cbw + 2 * W);
-    const int tv = W == rows - 1 ? st.top[sl] : 0;
+    c.pn = *(const rp_v2u *)(st.cb + (size_t)sl * cbw + 2 * W);
+    c.tv = W == rows - 1 ? st.top[sl] : 0;
+    return c;
+}
+
+template <int NS, int PP>
+__device__ __forceinline__ void rp_codes_store(unsigned short *CODE, const RpCodes &cd, int t)
+{
+    constexpr int l = 1024 * PP, HP = l / 2, rows = l / 64;
+    if (t >= NS * rows) return;
+    const int i = t / rows, W = t % rows;
+    const rp_v2u pn = cd.pn;
     rp_v2u *dst = (rp_v2u *)(CODE + i * HP + 32 * W);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {   // 8 codes = 16 bytes per store
+    for (int c = 0; c < 4; ++c) {
         u64 w[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             u64 acc = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const int j = 8 * c + 4 * h + k, b = 2 * j;   // pair 32 W + j: limbs b, b+1 of the row
+                const int j = 8 * c + 4 * h + k, b = 2 * j;
                 const int c0 = (int)((pn.x >> b) & 1) - (int)((pn.y >> b) & 1);
                 int c1 = (int)((pn.x >> (b + 1)) & 1) - (int)((pn.y >> (b + 1)) & 1);
-                c1 += j == 31 ? tv : 0;
+                c1 += j == 31 ? cd.tv : 0;
                 acc |= (u64)((c0 & 0xff) | ((c1 & 0xff) << 8)) << (16 * k);
             }
             w[h] = acc;
@@ -584,8 +605,9 @@ __global__ __launch_bounds__(rp_nt(1024 * PP, LOGG, DIR), 4) void k_rpass(PassAr
     unsigned short *CODE = (unsigned short *)smem;   // G HP codes (over the exchange slots)
     Pr x[G][R];
     if (!SPLIT) {
-        rp_stage_codes<G, PP>(CODE, st, SLT, t);
+        const RpCodes cd = rp_codes_load<G, PP>(st, SLT, t);   // masks first, limbs behind them
         rp_load_limbs<G, G, PP, NT>(x, st, SLT, t);
+        rp_codes_store<G, PP>(CODE, cd, t);
         __syncthreads();
         rp_decode<G, G, PP, NT>(x, CODE, t);
     } else {   // first forward column pass: FFT_split_bits fused into the load
@@ -727,8 +749,9 @@ __global__ __launch_bounds__(RP_NT) void k_rpair(PairArgs a)
     st.top = a.top;
     unsigned short *CODE = (unsigned short *)smem;
     Pr x[2][PP];
-    rp_stage_codes<LOADB ? 2 : 1, PP>(CODE, st, SL, t);
+    const RpCodes cd = rp_codes_load<LOADB ? 2 : 1, PP>(st, SL, t);
     rp_load_limbs<LOADB ? 2 : 1, 2, PP>(x, st, SL, t);
+    rp_codes_store<LOADB ? 2 : 1, PP>(CODE, cd, t);
     __syncthreads();
     rp_decode<LOADB ? 2 : 1, 2, PP>(x, CODE, t);
     // y <- 2^E y through exchange slot 0 (E workgroup-uniform); barriers on both sides
@@ -819,8 +842,9 @@ __global__ __launch_bounds__(RP_NT) void k_rchain(PairArgs a)
     st.top = a.top;
     unsigned short *CODE = (unsigned short *)smem;
     Pr x[NS][PP];
-    rp_stage_codes<NS, PP>(CODE, st, SL, t);
+    const RpCodes cd = rp_codes_load<NS, PP>(st, SL, t);
     rp_load_limbs<NS, NS, PP>(x, st, SL, t);
+    rp_codes_store<NS, PP>(CODE, cd, t);
     __syncthreads();
     rp_decode<NS, NS, PP>(x, CODE, t);
 #pragma unroll
@@ -988,8 +1012,9 @@ __global__ __launch_bounds__(NT) void k_rscale(u64 *dig, u64 *cb, int *top, u32 
     st.top = top;
     unsigned short *CODE = (unsigned short *)smem;
     Pr x[1][R];
-    rp_stage_codes<1, PP>(CODE, st, SL, t);
+    const RpCodes cd = rp_codes_load<1, PP>(st, SL, t);
     rp_load_limbs<1, 1, PP, NT>(x, st, SL, t);
+    rp_codes_store<1, PP>(CODE, cd, t);
     __syncthreads();
     rp_decode<1, 1, PP, NT>(x, CODE, t);
     rp_pub<PP, NT>(X, 0, x[0], t);
