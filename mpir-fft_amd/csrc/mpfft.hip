@@ -329,14 +329,15 @@ struct Exec {
     // level leaves no pending exponent (its pass skips the closing round) -- so the stage API
     // and the sharded path run the same passes.
     bool carry_pend = !diag_env("MPFFT_NO_CARRY");
-    // which hand-overs: 1 column -> column, 4 row -> row.  A hand-over into a plain pass moves
-    // that pass's first level from registers to an LDS round, about what the skipped closing
-    // round costs: measured (profiles/r03/carry_ab.txt) row -> row pays at l = 2048 and 4096,
-    // column -> column only at l = 4096 (C3 columns 2.02 -> 2.08 ms with it, C4 20.7 -> 19.9 ms).
+    // which hand-overs: 1 column -> column, 4 row -> row.  The receiving pass applies the
+    // owed exponents (whole limb pairs) by a rotated load -- addresses and a negation, no LDS
+    // round -- so its first level stays in registers and the skipped closing round is saved
+    // outright.  (Round 3, when the first level took the exponents through LDS instead, the
+    // hand-over paid only row -> row and column -> column at l = 4096: profiles/r03/carry_ab.txt.)
     int carry_mask() const
     {
         static const int m = [] { const char *e = diag_env("MPFFT_CARRY_MASK"); return e ? atoi(e) : -1; }();
-        return m >= 0 ? m : P.l >= 4096 ? 5 : 4;
+        return m >= 0 ? m : 5;
     }
     struct Fill { long lo = 0, off = 0; u64 rho = 0; bool done = false; } fill;   // itft's FILL, see ifft_block
     long dbl_lo = 0, dbl_hi = 0;
@@ -670,7 +671,7 @@ struct Exec {
 
     int fwd_columns_range(const u64 *srcA, long nA, const u64 *srcB, long nB, int nops, int op = -1)
     {
-        int lvl = 0, pend0 = 0;   // the data still owe the pending exponents of levels [pend0, lvl)
+        int lvl = 0, pend0 = 0;   // the data owe the pending exponents of levels [pend0, lvl)
         while (lvl < P.lbR) {
             PassArgs a = col_pass_args(lvl);
             if (lvl == 0) {
@@ -687,13 +688,15 @@ struct Exec {
             if (carry_pend && rp_mode(a, k, 0) >= 0 && (carry_mask() & 1) && lvl + k < P.lbR) {
                 const int k2 = split(P.lbR - lvl - k, true);
                 PassArgs n = col_pass_args(lvl + k);
-                n.pcarry = lvl + k - pend0;
+                n.pcarry = k;   // it would owe this pass's levels
                 a.pkeep = rp_mode(n, k2, 0) >= 0;
             }
             int rc = op < 0 ? pass(a, k, 0, nops) : pass(only(a, op), k, 0, 1);
             if (rc) return rc;
+            // a keeping pass owes its own levels only (a receiving pass applies what it was
+            // owed on load: rotated load, k_rpass MODE 3)
+            pend0 = a.pkeep ? lvl : lvl + k;
             lvl += k;
-            if (!a.pkeep) pend0 = lvl;
         }
         return MPFFT_OK;
     }
@@ -735,13 +738,15 @@ struct Exec {
             if (carry_pend && (carry_mask() & 4) && lvl + k < L && rp_mode(a, k, 0) >= 0) {
                 const int k2 = split(L - lvl - k);
                 PassArgs n = row_pass_args(lvl + k, k2, L);
-                n.pcarry = lvl + k - pend0;
+                n.pcarry = k;   // it would owe this pass's levels
                 a.pkeep = rp_mode(n, k2, 0) >= 0;
             }
             int rc = op < 0 ? pass(a, k, 0, nops) : pass(only(a, op), k, 0, 1);
             if (rc) return rc;
+            // a keeping pass owes its own levels only (a receiving pass applies what it was
+            // owed on load: rotated load, k_rpass MODE 3)
+            pend0 = a.pkeep ? lvl : lvl + k;
             lvl += k;
-            if (!a.pkeep) pend0 = lvl;
         }
         return MPFFT_OK;
     }

@@ -401,10 +401,21 @@ __device__ __forceinline__ void pw_load_piece(u64 (&L)[M], int &T, const u64 *di
         const int Wl = (l - 1) >> 6, bl = (l - 1) & 63;
         cin = -((int)((cbp[2 * Wl] >> bl) & 1) - (int)((cbp[2 * Wl + 1] >> bl) & 1)) - top;
     }
+    // the piece's LP limbs as 16-byte loads (m0 even, slots 64-byte aligned): LP / 2 vector
+    // loads per lane instead of LP 8-byte ones
+    typedef unsigned long long pw_v2u __attribute__((ext_vector_type(2)));
+    static_assert(LP % 2 == 0, "pieces of whole limb pairs");
+    u64 dv[LP];
+#pragma unroll
+    for (int j = 0; j < LP; j += 2) {
+        const pw_v2u q = *(const pw_v2u *)(dig + m0 + j);
+        dv[j] = q.x;
+        dv[j + 1] = q.y;
+    }
     i64 c = cin;   // signed carry into the next limb
 #pragma unroll
     for (int j = 0; j < LP; ++j) {
-        const u64 v = dig[m0 + j];
+        const u64 v = dv[j];
         const int k = j ? (int)((pw >> (b0 + j - 1)) & 1) - (int)((nw >> (b0 + j - 1)) & 1) : 0;
         const i64 add = c + k;        // |add| <= 4
         const u64 r = v + (u64)add;

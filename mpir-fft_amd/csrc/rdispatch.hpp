@@ -46,7 +46,9 @@ inline int rp_maxlogg_dit(int l) { return l == 2048 ? 4 : rp_maxlogg(l); }
 inline size_t rp_lds(int l, int logg)
 {
     const int G = 1 << logg, NX = G / 2 > 2 ? G / 2 : 2;
-    return (size_t)NX * 9 * l + 4 * (size_t)(3 * G + (G / 2) * logg);   // + exponent and slot tables
+    const int nt = rp_nt(l, logg, 0), R = 512 * (l / 1024) / nt;
+    return (size_t)NX * 9 * l + 4 * (size_t)(3 * G + (G / 2) * logg)   // + exponent and slot tables
+           + 20 * (size_t)(nt / 64) * G * R;                            // + rp_shift_all's edge table
 }
 
 // k_rpair<PP, OP>: the truncated inverse's pair steps (OP_DOUBLE .. OP_IBFLY, kernels.hpp)

@@ -258,6 +258,71 @@ __device__ __forceinline__ Pr rp_get_rot(const RX<PP> &X, int j, int pp, u32 e, 
     }
 }
 
+// The bit part of a general rotation on values already rotated by whole pairs (rotated
+// load): pair pp of 2^d z = lo(z_pp) + hi(z_(pp-1)) (pair 0: minus hi(z_(HP-1))), as rp_get_rot,
+// with z_(pp-1) taken from the register of lane - 1 (DPP wave_ror:1) -- no publish of the
+// coefficients.  Lane 0 of each wave needs lane 63 of the wave below (pair pp - 1 = thread
+// t - 1; thread 0 of round r: thread NT - 1 of round r - 1, round 0: pair HP - 1): those
+// lanes' pairs go through a small LDS table EDGE (NT/64 x G x R x 5 words), one barrier.
+// d = e mod 128 = 32 B + s, workgroup-uniform per slot.
+#ifndef RP_GX_LOAD
+#define RP_GX_LOAD 1   // 0: the round-3 form (plain load, general rotation through LDS), A/B builds only
+#endif
+__device__ __forceinline__ u32 rp_ror1(u32 v) { return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x13C, 0xF, 0xF, false); }
+
+template <int G, int PP, int NT, typename EF>
+__device__ __forceinline__ void rp_shift_all(Pr (&x)[G][rp_r(PP, NT)], u32 *EDGE, EF ef, int t)
+{
+    constexpr int R = rp_r(PP, NT), NW = NT / 64;
+    const int lane = t & 63, wv = t >> 6;
+    if (lane == 63) {
+#pragma unroll
+        for (int i = 0; i < G; ++i)
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                u32 *q = EDGE + 5 * ((wv * G + i) * R + r);
+                q[0] = x[i][r].w[0];
+                q[1] = x[i][r].w[1];
+                q[2] = x[i][r].w[2];
+                q[3] = x[i][r].w[3];
+                q[4] = (u32)x[i][r].h;
+            }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+        const u32 d = ef(i) & 127;
+        if (d == 0) continue;   // workgroup-uniform
+        const u32 s = d & 31;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            RP_FENCE();
+            Pr b;
+            b.w[0] = rp_ror1(x[i][r].w[0]);
+            b.w[1] = rp_ror1(x[i][r].w[1]);
+            b.w[2] = rp_ror1(x[i][r].w[2]);
+            b.w[3] = rp_ror1(x[i][r].w[3]);
+            b.h = (int)rp_ror1((u32)x[i][r].h);
+            if (lane == 0) {
+                const int w2 = wv ? wv - 1 : NW - 1, r2 = wv ? r : (r ? r - 1 : R - 1);
+                const u32 *q = EDGE + 5 * ((w2 * G + i) * R + r2);
+                b.w[0] = q[0];
+                b.w[1] = q[1];
+                b.w[2] = q[2];
+                b.w[3] = q[3];
+                b.h = (int)q[4];
+            }
+            const bool wrap = t == 0 && r == 0;   // pair 0: minus hi(z_(HP-1))
+            switch (d >> 5) {   // workgroup-uniform
+            case 0: x[i][r] = rp_shift_pair<0>(x[i][r], b, s, wrap); break;
+            case 1: x[i][r] = rp_shift_pair<1>(x[i][r], b, s, wrap); break;
+            case 2: x[i][r] = rp_shift_pair<2>(x[i][r], b, s, wrap); break;
+            default: x[i][r] = rp_shift_pair<3>(x[i][r], b, s, wrap); break;
+            }
+        }
+    }
+}
+
 // Exponents in 32 bits: every one is reduced mod 2N < 2^20 (l <= 4096), and a level
 // twiddle (k_pass :212-229) is below N (SGPR pressure: the 64-bit forms spilled).
 __device__ __forceinline__ u32 rp_mod2n(u32 e, u32 N2)
@@ -328,11 +393,16 @@ __device__ __forceinline__ void rp_rot_all(Pr (&x)[G][rp_r(PP, NT)], const RX<PP
 // multipliers (MFA twiddle before a DIF pass, bp_post after a DIT pass); [G, 2G) the
 // pending exponent of each slot after the last DIF level (applied by one aligned
 // rotation round); then G/2 partner exponents per level at 2G + li G/2.
-template <int LOGG, int DIR, bool GX>
-__device__ __forceinline__ u32 rp_exp_entry(const PassArgs &a, const BGeo &g, int e, u32 N2, u32 cadd)
+template <int LOGG, int DIR, bool GX, bool CIN = false>
+__device__ __forceinline__ u32 rp_exp_entry(const PassArgs &a0, const BGeo &g, int e, u32 N2, u32 cadd)
 {
     constexpr int G = 1 << LOGG;
+    // CIN: the inputs owe the pending exponents of levels [lvl0 - pcarry, lvl0); entries [0, G)
+    // hold them (applied by the rotated load), and the pass then owes only its own levels
+    PassArgs a = a0;
+    if (CIN) a.pcarry = 0;
     if (e < G) {
+        if (CIN) return rp_pend_pos((u32)a0.rho, a0.lbM, a0.lvl0 - a0.pcarry, a0.lvl0, (u32)(g.pos0 + e * g.pstep), N2);
         if (!GX) return 0;
         return DIR == 0 ? (u32)bp_mod2n(g.tw0 + (u64)e * g.twst + cadd, N2) : (u32)bp_post(a, g, e, N2);
     }
@@ -458,6 +528,66 @@ __device__ __forceinline__ void rp_load_limbs(Pr (&x)[NSX][rp_r(PP, NT)], const 
 
 // codes -> pair form: limb 2pp's carry moves into limb 2pp+1, limb 2pp+1's (and the carry
 // limb) is the pair overflow h.  Ends with a barrier: CODE aliases the exchange slots.
+// Rotated load (k_rpass MODE 3): slot i is read already multiplied by 2^E_i, E_i a whole
+// number of limb pairs (< 2N, workgroup-uniform): pair pp of 2^E y is pair pp - Y of y
+// (Y = (E mod N) / 128), negated when that index wraps below 0 (2^N == -1) xor E >= N.  The
+// pair's code (its carries) travels with it; its overflow h keeps meaning "into the next
+// pair" in the rotated frame, including across the wrap (the negated top pair lands at Y - 1
+// and its overflow at Y, which is where -h 2^N times 2^(128 Y) belongs).  So the pending
+// exponents an earlier pass left behind cost no LDS round: addresses and one negation.
+__device__ __forceinline__ int rp_rot_src(int pp, u32 e, u32 N, int HP, bool &neg)
+{
+    const bool sg = e >= N;
+    int src = pp - (int)((sg ? e - N : e) >> 7);
+    const bool wr = src < 0;
+    src += wr ? HP : 0;
+    neg = wr != sg;
+    return src;
+}
+
+template <int NS, int NSX, int PP, int NT, typename EF>
+__device__ __forceinline__ void rp_load_limbs_rot(Pr (&x)[NSX][rp_r(PP, NT)], const Coef &st, const u32 *SL, EF ef,
+                                                  int t)
+{
+    constexpr int l = 1024 * PP, HP = l / 2;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        const long sl = (long)rp_uniform(SL[i]);
+        const u32 e = ef(i);
+#pragma unroll
+        for (int r = 0; r < rp_r(PP, NT); ++r) {
+            bool ng;
+            const int src = rp_rot_src(t + NT * r, e, (u32)(64 * l), HP, ng);
+            x[i][r] = pr_make(*(const rp_v4u *)(st.dig + (size_t)sl * l + 2 * src), 0);
+        }
+        RP_FENCE();   // a slot's addresses die with its loads (all loads stay in flight)
+    }
+}
+
+template <int NS, int NSX, int PP, int NT, typename EF>
+__device__ __forceinline__ void rp_decode_rot(Pr (&x)[NSX][rp_r(PP, NT)], const unsigned short *CODE, EF ef, int t)
+{
+    constexpr int HP = 512 * PP;
+    t = rp_launder(t);
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        const u32 e = ef(i);
+#pragma unroll
+        for (int r = 0; r < rp_r(PP, NT); ++r) {
+            RP_FENCE();
+            bool ng;
+            const int src = rp_rot_src(t + NT * r, e, (u32)(128 * HP), HP, ng);
+            const int code = CODE[i * HP + src];
+            const int c0 = (signed char)(code & 0xff), c1 = (signed char)(code >> 8);
+            int cc;
+            add_small(x[i][r].w[2], x[i][r].w[3], c0, cc);
+            x[i][r].h = c1 + cc;
+            x[i][r] = pr_cneg(x[i][r], ng);
+        }
+    }
+    __syncthreads();
+}
+
 template <int NS, int NSX, int PP, int NT = RP_NT>
 __device__ __forceinline__ void rp_decode(Pr (&x)[NSX][rp_r(PP, NT)], const unsigned short *CODE, int t)
 {
@@ -539,7 +669,8 @@ __device__ __forceinline__ void rp_pin(Pr (&x)[G][R])
 
 // MODE: DIR 0: 0 plain, 1 MFA twiddle on load, 2 split on load (first column pass),
 //               3 plain with inputs that still owe an earlier pass's pending exponents
-//               (PassArgs::pcarry: the first level rotates its partners through LDS too);
+//               (PassArgs::pcarry: applied by a rotated load, rp_load_limbs_rot, so the
+//               first level still runs in registers);
 //       DIR 1: bit 0 general final multipliers (inverse twiddle / scaling), bit 1 the pass
 //               holds the transform's last DIT level (h = 1: its first level needs no rotation),
 //               bit 2 the truncated inverse's FILL step (PassArgs::fill_*; not with bit 0)
@@ -592,7 +723,7 @@ __global__ __launch_bounds__(rp_nt(1024 * PP, LOGG, DIR), 4) void k_rpass(PassAr
     constexpr int NEXP = 2 * G + (G / 2) * LOGG;
     u32 *EXPT = (u32 *)(smem + NX * RX<PP>::SB);
     u32 *SLT = EXPT + NEXP;
-    if (t < NEXP) EXPT[t] = rp_exp_entry<LOGG, DIR, GX>(a, g, t, N2, 0u);
+    if (t < NEXP) EXPT[t] = rp_exp_entry<LOGG, DIR, GX, CIN>(a, g, t, N2, 0u);
     else if (t < NEXP + G) SLT[t - NEXP] = (u32)slot_lane(t - NEXP);
     __syncthreads();
     const u64 *src = SPLIT ? a.src[op] : nullptr;
@@ -604,7 +735,26 @@ __global__ __launch_bounds__(rp_nt(1024 * PP, LOGG, DIR), 4) void k_rpass(PassAr
     // ---- load ------------------------------------------------------------------------
     unsigned short *CODE = (unsigned short *)smem;   // G HP codes (over the exchange slots)
     Pr x[G][R];
-    if (!SPLIT) {
+    u32 *EDGE = SLT + G;   // rp_shift_all's lane-63 table (rp_lds)
+    if (DIR == 0 && GX && RP_GX_LOAD) {   // MFA twiddle 2^(tw0 + s twst) of slot s (README:89), so every level is pair-aligned:
+        // whole pairs by the rotated load, the rest by neighbour pairs in registers
+        auto ef = [&](int i) -> u32 { return rp_uniform(EXPT[i]); };
+        const RpCodes cd = rp_codes_load<G, PP>(st, SLT, t);
+        rp_load_limbs_rot<G, G, PP, NT>(x, st, SLT, ef, t);
+        rp_codes_store<G, PP>(CODE, cd, t);
+        __syncthreads();
+        rp_decode_rot<G, G, PP, NT>(x, CODE, ef, t);
+        rp_pin<G, R>(x);
+        rp_shift_all<G, PP, NT>(x, EDGE, ef, t);
+    } else if (CIN) {   // owed pending exponents: rotated load (EXPT[0, G))
+        auto ef = [&](int i) -> u32 { return rp_uniform(EXPT[i]); };
+        const RpCodes cd = rp_codes_load<G, PP>(st, SLT, t);
+        rp_load_limbs_rot<G, G, PP, NT>(x, st, SLT, ef, t);
+        rp_codes_store<G, PP>(CODE, cd, t);
+        __syncthreads();
+        rp_decode_rot<G, G, PP, NT>(x, CODE, ef, t);
+        rp_pin<G, R>(x);   // the rotated values materialised before the register level (else spills)
+    } else if (!SPLIT) {
         const RpCodes cd = rp_codes_load<G, PP>(st, SLT, t);   // masks first, limbs behind them
         rp_load_limbs<G, G, PP, NT>(x, st, SLT, t);
         rp_codes_store<G, PP>(CODE, cd, t);
@@ -638,7 +788,7 @@ __global__ __launch_bounds__(rp_nt(1024 * PP, LOGG, DIR), 4) void k_rpass(PassAr
         }
     }
     RP_STAMP(1);
-    if (DIR == 0 && GX) {   // MFA twiddle 2^(tw0 + s twst) of slot s (README:89), so every level is pair-aligned
+    if (DIR == 0 && GX && !RP_GX_LOAD) {   // (A/B variant) the MFA twiddle through LDS after a plain load
         rp_rot_all<G, PP, NX, NT>(x, X, [&](int s) -> u32 { return rp_uniform(EXPT[s]); }, N, t);
     }
 
@@ -650,7 +800,7 @@ __global__ __launch_bounds__(rp_nt(1024 * PP, LOGG, DIR), 4) void k_rpass(PassAr
         // exponents yet, rp_pend(.., 0, ..) == 0, unless an earlier pass left its own) and the
         // first DIT level of the pass that holds the transform's last level (h == 1: rp_tw == 0).
         // Partners are then this thread's own registers -- no LDS round (workgroup-uniform).
-        if ((DIR == 0 && li == 0 && !CIN) || (DIR == 1 && li == 0 && HL)) {
+        if ((DIR == 0 && li == 0) || (DIR == 1 && li == 0 && HL)) {
 #pragma unroll
             for (int pi = 0; pi < G / 2; ++pi) {
                 const int i = ((pi >> JB) << (JB + 1)) | (pi & ((1 << JB) - 1));
