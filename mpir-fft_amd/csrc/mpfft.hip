@@ -584,21 +584,12 @@ struct Exec {
     PassArgs col_args() const
     {
         PassArgs a = base_args(col);
-        if (cb0) {   // a batch of columns [cb0, cb0 + cbn) (fwd_columns)
-            const long cbw = cb_words((int)P.l);
-            for (int k = 0; k < 2; ++k) {
-                a.dig[k] += (long)cb0 * P.l;
-                a.cb[k] += (long)cb0 * cbw;
-                a.top[k] += cb0;
-            }
-        }
         a.sub_stride = 1;
         a.pos_stride = ccount;
-        a.nsub = cbn ? cbn : ccount;
-        a.sub_off = c0 + cb0;
+        a.nsub = ccount;
+        a.sub_off = c0;
         return a;
     }
-    int cb0 = 0, cbn = 0;   // column batch of the forward column passes (0, 0: every column)
 
     // row layout passes over this rank's rcount rows
     PassArgs row_args() const
@@ -650,26 +641,7 @@ struct Exec {
         return a;
     }
 
-    // Column batches (diagnostics, MPFFT_COL_BATCH=b): all forward column passes of b columns
-    // before the next b -- with b columns of both operands within the 256 MiB Infinity Cache,
-    // only the first read and the last write of a batch reach HBM
     int fwd_columns(const u64 *srcA, long nA, const u64 *srcB, long nB, int nops, int op = -1)
-    {
-        static const int B = [] { const char *e = diag_env("MPFFT_COL_BATCH"); return e ? atoi(e) : 0; }();
-        if (B <= 0 || B >= ccount || src_chunk) return fwd_columns_range(srcA, nA, srcB, nB, nops, op);
-        u32 *zp = zflags;
-        int rc = MPFFT_OK;
-        for (cb0 = 0; cb0 < ccount && !rc; cb0 += B) {
-            cbn = ccount - cb0 < B ? ccount - cb0 : B;
-            rc = fwd_columns_range(srcA, nA, srcB, nB, nops, op);
-            zflags = nullptr;   // cleared by the first batch's first pass
-        }
-        zflags = zp;
-        cb0 = cbn = 0;
-        return rc;
-    }
-
-    int fwd_columns_range(const u64 *srcA, long nA, const u64 *srcB, long nB, int nops, int op = -1)
     {
         int lvl = 0, pend0 = 0;   // the data owe the pending exponents of levels [pend0, lvl)
         while (lvl < P.lbR) {

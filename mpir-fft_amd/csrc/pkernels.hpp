@@ -388,35 +388,61 @@ __device__ __forceinline__ void pw_transform(u64 (&L)[M], int &T, int &S, unsign
 // L + T 2^N', T in {-1, 0}: the convolution tolerates such pieces (|c_t| < K 2^(2B+1)
 // still fits the headroom N' >= 2B + lk + 4, pdispatch.hpp), so the pointwise inputs need no
 // canonicalisation pass.  A piece lies inside one 64-limb mask row (LP | 64).
-template <int M, int LP>
-__device__ __forceinline__ void pw_load_piece(u64 (&L)[M], int &T, const u64 *dig, const u64 *cbp, int top, int l, int t)
+// The loads of a piece (its LP limbs, its own carry-mask words and those of the limb below
+// it, the slot's carry limb), issued before any of them is used (pw_piece_fetch), then the
+// arithmetic (pw_piece_make): a workgroup requests all its pieces' bytes at once and waits
+// one HBM round trip, where a load-compute-load order waited one per piece (the masks of
+// the limb below depend on nothing loaded, so nothing forces the order).
+template <int LP>
+struct PwRaw {
+    u64 v[LP];
+    u64 pw, nw;     // carry masks of the piece's 64-limb row
+    u64 pwp, nwp;   // of the row holding limb m0 - 1 (or l - 1 for piece 0)
+    int top;
+};
+
+template <int LP>
+__device__ __forceinline__ void pw_piece_fetch(PwRaw<LP> &R, const u64 *dig, const u64 *cbp, const int *topp, int l,
+                                               int t)
 {
-    const int m0 = t * LP, W = m0 >> 6, b0 = m0 & 63;
-    const u64 pw = cbp[2 * W], nw = cbp[2 * W + 1];
-    int cin;
-    if (m0) {
-        const int Wp = (m0 - 1) >> 6, bp = (m0 - 1) & 63;
-        cin = (int)((cbp[2 * Wp] >> bp) & 1) - (int)((cbp[2 * Wp + 1] >> bp) & 1);
-    } else {
-        const int Wl = (l - 1) >> 6, bl = (l - 1) & 63;
-        cin = -((int)((cbp[2 * Wl] >> bl) & 1) - (int)((cbp[2 * Wl + 1] >> bl) & 1)) - top;
-    }
-    // the piece's LP limbs as 16-byte loads (m0 even, slots 64-byte aligned): LP / 2 vector
-    // loads per lane instead of LP 8-byte ones
     typedef unsigned long long pw_v2u __attribute__((ext_vector_type(2)));
     static_assert(LP % 2 == 0, "pieces of whole limb pairs");
-    u64 dv[LP];
+    const int m0 = t * LP, W = m0 >> 6, mb = m0 ? m0 - 1 : l - 1, Wp = mb >> 6;
+    // the piece's LP limbs as 16-byte loads (m0 even, slots 64-byte aligned)
 #pragma unroll
     for (int j = 0; j < LP; j += 2) {
         const pw_v2u q = *(const pw_v2u *)(dig + m0 + j);
-        dv[j] = q.x;
-        dv[j + 1] = q.y;
+        R.v[j] = q.x;
+        R.v[j + 1] = q.y;
     }
+    const pw_v2u c = *(const pw_v2u *)(cbp + 2 * W), cp = *(const pw_v2u *)(cbp + 2 * Wp);
+    R.pw = c.x;
+    R.nw = c.y;
+    R.pwp = cp.x;
+    R.nwp = cp.y;
+    R.top = *topp;
+}
+
+// Piece t of a coefficient in the reduced HBM form (coeff.hpp: limbs + carry masks +
+// carry limb): limbs [t LP, t LP + LP) plus the carries into them -- the carry out of
+// limb m lands in limb m + 1, the carry into limb 0 is minus the carry out of limb l-1
+// and minus the carry limb (both weigh 2^N == -1); the carry out of the piece's top limb
+// is the next piece's.  The value v (-2 <= v < 2^(64 LP) + 2^(64 LP - 64)) is returned as
+// L + T 2^N', T in {-1, 0}: the convolution tolerates such pieces (|c_t| < K 2^(2B+1)
+// still fits the headroom N' >= 2B + lk + 4, pdispatch.hpp), so the pointwise inputs need no
+// canonicalisation pass.  A piece lies inside one 64-limb mask row (LP | 64).
+template <int M, int LP>
+__device__ __forceinline__ void pw_piece_make(u64 (&L)[M], int &T, const PwRaw<LP> &R, int l, int t)
+{
+    const int m0 = t * LP, b0 = m0 & 63;
+    const int mb = m0 ? m0 - 1 : l - 1, bp = mb & 63;
+    const int kb = (int)((R.pwp >> bp) & 1) - (int)((R.nwp >> bp) & 1);
+    const int cin = m0 ? kb : -kb - R.top;
     i64 c = cin;   // signed carry into the next limb
 #pragma unroll
     for (int j = 0; j < LP; ++j) {
-        const u64 v = dv[j];
-        const int k = j ? (int)((pw >> (b0 + j - 1)) & 1) - (int)((nw >> (b0 + j - 1)) & 1) : 0;
+        const u64 v = R.v[j];
+        const int k = j ? (int)((R.pw >> (b0 + j - 1)) & 1) - (int)((R.nw >> (b0 + j - 1)) & 1) : 0;
         const i64 add = c + k;        // |add| <= 4
         const u64 r = v + (u64)add;
         c = add >= 0 ? (i64)(r < v) : -(i64)(r > v);
@@ -428,6 +454,15 @@ __device__ __forceinline__ void pw_load_piece(u64 (&L)[M], int &T, const u64 *di
 #pragma unroll
     for (int j = LP; j < M; ++j) L[j] = j == LP ? (c > 0 ? 1ull : up) : up;
     T = c < 0 ? -1 : 0;
+}
+
+template <int M, int LP>
+__device__ __forceinline__ void pw_load_piece(u64 (&L)[M], int &T, const u64 *dig, const u64 *cbp, const int *topp,
+                                              int l, int t)
+{
+    PwRaw<LP> R;
+    pw_piece_fetch<LP>(R, dig, cbp, topp, l, t);
+    pw_piece_make<M, LP>(L, T, R, l, t);
 }
 
 // limbs per piece of the instantiated k_pwss shapes: l / K (l = 1024: M = 10, LP = 4;
@@ -447,8 +482,13 @@ __device__ __forceinline__ void pw_load_pair_bfly(u64 (&L)[M], int &T, const u64
 {
     u64 A[M], B[M];
     int Ta, Tb;
-    pw_load_piece<M, LP>(A, Ta, dig + (size_t)s0 * l, cb + (size_t)s0 * cbw, top[s0], l, t);
-    pw_load_piece<M, LP>(B, Tb, dig + (size_t)(s0 + 1) * l, cb + (size_t)(s0 + 1) * cbw, top[s0 + 1], l, t);
+    {
+        PwRaw<LP> RA, RB;   // both slots' bytes requested before either is used
+        pw_piece_fetch<LP>(RA, dig + (size_t)s0 * l, cb + (size_t)s0 * cbw, top + s0, l, t);
+        pw_piece_fetch<LP>(RB, dig + (size_t)(s0 + 1) * l, cb + (size_t)(s0 + 1) * cbw, top + s0 + 1, l, t);
+        pw_piece_make<M, LP>(A, Ta, RA, l, t);
+        pw_piece_make<M, LP>(B, Tb, RB, l, t);
+    }
     // limbs LP .. M-1 of A, B are the sign extension (carry limb LP, then 0 / ~0): add LP + 1 limbs
     const u32 m = sub ? ~0u : 0u;
     u32 c = sub ? 1u : 0u;
@@ -624,8 +664,13 @@ __global__ __launch_bounds__(1 << LK) __attribute__((amdgpu_waves_per_eu(pw_wpe<
     int Ta, Tb;
     if (FUSE == 0) {
         const long slot = blockIdx.x;
-        pw_load_piece<M, CLP>(La, Ta, digA + (size_t)slot * l, cbA + (size_t)slot * cbw, topA[slot], l, t);
-        pw_load_piece<M, CLP>(Lb, Tb, digB + (size_t)slot * l, cbB + (size_t)slot * cbw, topB[slot], l, t);
+        {
+            PwRaw<CLP> RA, RB;   // both operands' bytes requested before either is used
+            pw_piece_fetch<CLP>(RA, digA + (size_t)slot * l, cbA + (size_t)slot * cbw, topA + slot, l, t);
+            pw_piece_fetch<CLP>(RB, digB + (size_t)slot * l, cbB + (size_t)slot * cbw, topB + slot, l, t);
+            pw_piece_make<M, CLP>(La, Ta, RA, l, t);
+            pw_piece_make<M, CLP>(Lb, Tb, RB, l, t);
+        }
         __syncthreads();   // every piece read before any output limb is written (in place on A)
         pw_slot_product<M, LK>(La, Ta, Lb, Tb, X, Xw, TT, PP, t, stamp);
         pw_slot_output<M, LK>(X, TT, H, digA + (size_t)slot * l, cbA + (size_t)slot * cbw, topA + slot, l, t);
