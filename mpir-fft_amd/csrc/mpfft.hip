@@ -135,7 +135,7 @@ static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // sqrt2: the new_mpn_mul6 front end (mul_fft.c:3573-3603): a length-4n convolution with
 // bits1 = (N - (depth + 1))/2 (:3578) and the same trunc rule (:3603)
-static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned long w, bool sqrt2 = false)
+static int make_plan_split(Plan *p, long n1, long n2, unsigned long depth, unsigned long w, bool sqrt2, int lbc)
 {
     memset(p, 0, sizeof(*p));
     p->sqrt2 = sqrt2;
@@ -153,7 +153,7 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
     if (sqrt2 && p->N <= depth + 1) return MPFFT_EINVAL;
     p->bits1 = (p->N - depth - (sqrt2 ? 1 : 0)) / 2;
     if (p->bits1 < 1) return MPFFT_EINVAL;
-    p->NC = 1L << (depth / 2);
+    p->NC = 1L << (lbc >= 0 ? lbc : (int)depth / 2);   // the reference's split (mul_fft.c:3195) unless make_plan picks another
     p->NR = 2 * p->n / p->NC;
     p->lbC = ilog2(p->NC);
     p->lbR = ilog2(p->NR);
@@ -235,7 +235,8 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
     {
         const int ml = p->maxlogg > 0 ? p->maxlogg : 1;
         const bool saves = (p->lbC - 1 + ml - 1) / ml < (p->lbC + ml - 1) / ml;
-        p->has_c = p->lbC >= 2 && saves && pw_pair_kernel(p->l);
+        // four-level row passes: the fused level also shortens the last pass (8 = 4 + 4 -> 4 + 3)
+        p->has_c = p->lbC >= 2 && (saves || ml >= 4) && pw_pair_kernel(p->l);
     }
     if (p->has_c) {
         p->off_digC = o; o += dig;
@@ -244,6 +245,36 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
     }
     p->off_flags = o; o += align_up((size_t)(p->total / 256 + 8) * 4, 256);   // k_combine1 blocks at V = 1
     p->bytes = o;
+    return MPFFT_OK;
+}
+
+// Pass-operand cost of a plan's transforms, for the matrix split below: forward passes move
+// both operands, inverse ones the product, the pointwise ~5.5 pass-equivalents per slot
+// (C3: 3.5 ms against 0.64 ms per forward pass of both operands); all per live slot.
+static double plan_cost(const Plan &P)
+{
+    auto np = [](int lev, int ml) { return ml > 0 ? (lev + ml - 1) / ml : lev; };
+    const int ml = P.maxlogg, mlc = P.maxlogg_c ? P.maxlogg_c : ml, mli = P.maxlogg_i ? P.maxlogg_i : ml;
+    const int fwd = np(P.lbR, mlc) + np(P.lbC - (P.has_c ? 1 : 0), ml), inv = np(P.lbC, mli) + np(P.lbR, mli);
+    return (double)P.trunc * (2.0 * fwd + inv + 2 * 5.5);
+}
+
+// The matrix split of the MFA is internal (no internal ABI): the reference takes
+// NC = 2^floor(depth/2) columns (mul_fft.c:3195); with the register-resident passes (three
+// levels per forward pass) one more column level can save a whole pass -- C4 (depth 17):
+// 256 x 1024 needs 4 + 3 forward passes (10 = 3+3+2+2 column levels, 8 row levels), 512 x 512
+// needs 3 + 3.  Both splits give the same exact product; the cheaper one is taken.
+static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned long w, bool sqrt2 = false)
+{
+    int rc = make_plan_split(p, n1, n2, depth, w, sqrt2, -1);
+    static const bool ref_split = diag_env("MPFFT_REF_SPLIT") != nullptr;   // diagnostics: A/B
+    // only where measured to pay: four-level forward passes at l = 2048 (C4's 512 x 512 split
+    // with three-level passes measured slower, profiles/r04/mfa_split_ab.txt)
+    if (rc || sqrt2 || !p->rpass || ref_split || rp_maxlogg((int)p->l) < 4) return rc;
+    Plan q;
+    if (make_plan_split(&q, n1, n2, depth, w, sqrt2, (int)depth / 2 + 1) == MPFFT_OK && q.rpass &&
+        plan_cost(q) < plan_cost(*p))
+        *p = q;
     return MPFFT_OK;
 }
 
