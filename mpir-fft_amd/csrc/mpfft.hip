@@ -135,7 +135,9 @@ static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // sqrt2: the new_mpn_mul6 front end (mul_fft.c:3573-3603): a length-4n convolution with
 // bits1 = (N - (depth + 1))/2 (:3578) and the same trunc rule (:3603)
-static int make_plan_split(Plan *p, long n1, long n2, unsigned long depth, unsigned long w, bool sqrt2, int lbc)
+// lbc >= 0: NC = 2^lbc instead of the reference's split; fwd4: four-level forward k_rpass passes
+static int make_plan_split(Plan *p, long n1, long n2, unsigned long depth, unsigned long w, bool sqrt2, int lbc,
+                           bool fwd4 = false)
 {
     memset(p, 0, sizeof(*p));
     p->sqrt2 = sqrt2;
@@ -209,7 +211,7 @@ static int make_plan_split(Plan *p, long n1, long n2, unsigned long depth, unsig
         const char *er = diag_env("MPFFT_RPASS");
         p->rpass = rp_maxlogg((int)p->l) > 0 && !(er && !strcmp(er, "0")) && !diag_env("MPFFT_BP_STAMPS");
         if (p->rpass && !e) {   // same levels per pass for columns and rows (two groups per CU either way)
-            int rl = rp_maxlogg((int)p->l);   // register-resident: not bound by k_bpass's LDS fit
+            int rl = fwd4 ? rp_maxlogg_fwd4((int)p->l) : rp_maxlogg((int)p->l);   // register-resident: not bound by k_bpass's LDS fit
             const char *ec = diag_env("MPFFT_RPLOGG");   // diagnostics: fewer levels per pass (A/B)
             if (ec && atoi(ec) >= 1 && atoi(ec) < rl) rl = atoi(ec);
             p->maxlogg = p->maxlogg_c = rl;
@@ -235,8 +237,7 @@ static int make_plan_split(Plan *p, long n1, long n2, unsigned long depth, unsig
     {
         const int ml = p->maxlogg > 0 ? p->maxlogg : 1;
         const bool saves = (p->lbC - 1 + ml - 1) / ml < (p->lbC + ml - 1) / ml;
-        // four-level row passes: the fused level also shortens the last pass (8 = 4 + 4 -> 4 + 3)
-        p->has_c = p->lbC >= 2 && (saves || ml >= 4) && pw_pair_kernel(p->l);
+        p->has_c = p->lbC >= 2 && saves && pw_pair_kernel(p->l);
     }
     if (p->has_c) {
         p->off_digC = o; o += dig;
@@ -248,33 +249,23 @@ static int make_plan_split(Plan *p, long n1, long n2, unsigned long depth, unsig
     return MPFFT_OK;
 }
 
-// Pass-operand cost of a plan's transforms, for the matrix split below: forward passes move
-// both operands, inverse ones the product, the pointwise ~5.5 pass-equivalents per slot
-// (C3: 3.5 ms against 0.64 ms per forward pass of both operands); all per live slot.
-static double plan_cost(const Plan &P)
-{
-    auto np = [](int lev, int ml) { return ml > 0 ? (lev + ml - 1) / ml : lev; };
-    const int ml = P.maxlogg, mlc = P.maxlogg_c ? P.maxlogg_c : ml, mli = P.maxlogg_i ? P.maxlogg_i : ml;
-    const int fwd = np(P.lbR, mlc) + np(P.lbC - (P.has_c ? 1 : 0), ml), inv = np(P.lbC, mli) + np(P.lbR, mli);
-    return (double)P.trunc * (2.0 * fwd + inv + 2 * 5.5);
-}
-
 // The matrix split of the MFA is internal (no internal ABI): the reference takes
-// NC = 2^floor(depth/2) columns (mul_fft.c:3195); with the register-resident passes (three
-// levels per forward pass) one more column level can save a whole pass -- C4 (depth 17):
-// 256 x 1024 needs 4 + 3 forward passes (10 = 3+3+2+2 column levels, 8 row levels), 512 x 512
-// needs 3 + 3.  Both splits give the same exact product; the cheaper one is taken.
+// NC = 2^floor(depth/2) columns (mul_fft.c:3195).  At l = 2048 with truncation case b
+// (trunc > half the convolution) twice the columns with four-level forward passes is faster:
+// C3 (depth 15) 256 x 256 runs its 8 column levels in 4 + 4 where 128 x 512 needs 3 + 3 + 3,
+// 8.64 vs 8.81 ms; in case a the reference split's column transform skips its empty upper
+// half and wins (C2: 6.69 vs 6.99 ms); at l = 4096 (C4) 512 x 512 with three-level passes
+// measured slower (97.1 vs 96.2 ms).  profiles/r04/mfa_split_ab.txt.  Both splits give the
+// same exact product.
 static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned long w, bool sqrt2 = false)
 {
     int rc = make_plan_split(p, n1, n2, depth, w, sqrt2, -1);
-    static const bool ref_split = diag_env("MPFFT_REF_SPLIT") != nullptr;   // diagnostics: A/B
-    // only where measured to pay: four-level forward passes at l = 2048 (C4's 512 x 512 split
-    // with three-level passes measured slower, profiles/r04/mfa_split_ab.txt)
-    if (rc || sqrt2 || !p->rpass || ref_split || rp_maxlogg((int)p->l) < 4) return rc;
+    // diagnostics (A/B): MPFFT_SPLIT=ref / alt forces a split
+    static const char *force = diag_env("MPFFT_SPLIT");
+    if (rc || sqrt2 || !p->rpass || p->l != 2048 || (force && !strcmp(force, "ref"))) return rc;
+    if (!(force && !strcmp(force, "alt")) && 2 * p->Tr <= p->NR) return rc;
     Plan q;
-    if (make_plan_split(&q, n1, n2, depth, w, sqrt2, (int)depth / 2 + 1) == MPFFT_OK && q.rpass &&
-        plan_cost(q) < plan_cost(*p))
-        *p = q;
+    if (make_plan_split(&q, n1, n2, depth, w, sqrt2, (int)depth / 2 + 1, true) == MPFFT_OK && q.rpass) *p = q;
     return MPFFT_OK;
 }
 
@@ -449,7 +440,7 @@ struct Exec {
     // split, or some level rotation is not a whole number of limb pairs
     int rpass_mode(const PassArgs &a, int logg, int dir) const
     {
-        if (!P.rpass || logg > (dir ? rp_maxlogg_dit((int)P.l) : rp_maxlogg((int)P.l)) || a.canon || a.rho % 128) return -1;
+        if (!P.rpass || logg > (dir ? rp_maxlogg_dit((int)P.l) : rp_maxlogg_fwd4((int)P.l)) || a.canon || a.rho % 128) return -1;
         if (dir == 0) {
             if (a.scale_e || a.tw_mode == 2) return -1;
             if (a.src[0] || a.src[1]) return a.tw_mode || a.pcarry ? -1 : 2;

@@ -37,11 +37,10 @@ rp_fn rp_get(int l, int logg, int dir, int mode);
 
 // most levels per pass: 32 limbs per thread (G l <= 16384 limbs per 512-thread workgroup,
 // 32768 at l = 4096 with 1024 threads)
-#ifndef RP_FWD4
-#define RP_FWD4 0   // 1: four-level forward passes at l = 2048 (1024 threads, one workgroup per CU)
-#endif
-inline int rp_maxlogg(int l) { return l == 1024 ? 3 : l == 2048 ? (RP_FWD4 ? 4 : 3) : l == 4096 ? 3 : 0; }   // l = 1024: G = 16 spills
-// inverse (DIT) passes: four levels at l = 2048 (1024 threads, one workgroup per CU)
+inline int rp_maxlogg(int l) { return l == 1024 ? 3 : l == 2048 ? 3 : l == 4096 ? 3 : 0; }   // l = 1024: G = 16 spills
+// forward passes of four levels at l = 2048 (1024 threads, one workgroup per CU): built, and
+// taken by the plans whose MFA split make_plan chooses for them
+inline int rp_maxlogg_fwd4(int l) { return l == 2048 ? 4 : rp_maxlogg(l); }
 inline int rp_maxlogg_dit(int l) { return l == 2048 ? 4 : rp_maxlogg(l); }
 
 // LDS: NX exchange slots of 9 l bytes (limbs + 16-bit pair overflows) and the exponent

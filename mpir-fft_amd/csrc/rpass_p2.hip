@@ -5,17 +5,10 @@ rp_fn rp_get_p2(int logg, int dir, int mode)
 {
     static const rp_fn tab[2][8][5] = {
         {
-#if RP_FWD4
             {nullptr, k_rpass<1, 2, 0, 0>, k_rpass<2, 2, 0, 0>, k_rpass<3, 2, 0, 0>, k_rpass<4, 2, 0, 0>},
             {nullptr, k_rpass<1, 2, 0, 1>, k_rpass<2, 2, 0, 1>, k_rpass<3, 2, 0, 1>, k_rpass<4, 2, 0, 1>},
             {nullptr, k_rpass<1, 2, 0, 2>, k_rpass<2, 2, 0, 2>, k_rpass<3, 2, 0, 2>, k_rpass<4, 2, 0, 2>},
             {nullptr, k_rpass<1, 2, 0, 3>, k_rpass<2, 2, 0, 3>, k_rpass<3, 2, 0, 3>, k_rpass<4, 2, 0, 3>},
-#else
-            {nullptr, k_rpass<1, 2, 0, 0>, k_rpass<2, 2, 0, 0>, k_rpass<3, 2, 0, 0>, nullptr},
-            {nullptr, k_rpass<1, 2, 0, 1>, k_rpass<2, 2, 0, 1>, k_rpass<3, 2, 0, 1>, nullptr},
-            {nullptr, k_rpass<1, 2, 0, 2>, k_rpass<2, 2, 0, 2>, k_rpass<3, 2, 0, 2>, nullptr},
-            {nullptr, k_rpass<1, 2, 0, 3>, k_rpass<2, 2, 0, 3>, k_rpass<3, 2, 0, 3>, nullptr},
-#endif
             {}, {}, {}, {},
         },
         {
