@@ -149,6 +149,8 @@ int mpfft_shard_row_fused(long n1, long n2, unsigned long depth, unsigned long w
 #define MPFFT_SHARD_POINTWISE 2     /* row layout A <- A * B */
 #define MPFFT_SHARD_INV_ROWS 3      /* row DIT + un-twiddle of A (row layout) */
 #define MPFFT_SHARD_INV_COLUMNS 4   /* truncated column inverse + scale of A (column layout), canonical */
+#define MPFFT_SHARD_FWD_COLUMNS_A 5 /* MPFFT_SHARD_FWD_COLUMNS for operand 1 only (clears the combine flags) */
+#define MPFFT_SHARD_FWD_COLUMNS_B 6 /* ... for operand 2 only: with _A, lets operand 1's exchange overlap it */
 int mpfft_shard_stage(int stage, const mpfft_shard *sh, const uint64_t *d_i1, const uint64_t *d_i2, void *stream);
 
 /* Combine the canonical coefficients of the row layout (A) into product limbs

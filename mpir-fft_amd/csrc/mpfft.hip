@@ -1595,6 +1595,8 @@ int mpfft_shard_stage(int stage, const mpfft_shard *sh, const uint64_t *d_i1, co
     if ((rc = shard_exec(X, sh))) return rc;
     switch (stage) {
     case MPFFT_SHARD_FWD_COLUMNS: return X.fwd_columns(d_i1, sh->n1, d_i2, sh->n2, 2);
+    case MPFFT_SHARD_FWD_COLUMNS_A: return X.fwd_columns(d_i1, sh->n1, d_i2, sh->n2, 2, 0);
+    case MPFFT_SHARD_FWD_COLUMNS_B: return X.fwd_columns(d_i1, sh->n1, d_i2, sh->n2, 2, 1);
     case MPFFT_SHARD_FWD_ROWS: return X.rcount ? X.fwd_rows(2) : MPFFT_OK;
     case MPFFT_SHARD_POINTWISE: return X.pointwise();
     case MPFFT_SHARD_INV_ROWS: return X.rcount ? X.inv_rows() : MPFFT_OK;

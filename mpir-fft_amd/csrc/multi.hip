@@ -124,6 +124,9 @@ struct Rank {
     int dev = 0;
     hipStream_t s = nullptr;
     hipEvent_t ev = nullptr;
+    hipStream_t xs = nullptr;    // exchange #1's copies (overlapping operand 2's column passes)
+    hipEvent_t eva = nullptr;    // operand 1's column passes done
+    hipEvent_t evx = nullptr;    // exchange #1 done
     unsigned char *mem = nullptr;
     size_t mem_bytes = 0;
     u64 *host = nullptr;      // pinned staging of the operand slices
@@ -155,8 +158,12 @@ void free_rank(Rank &R)
     }
     if (R.mem) (void)hipFree(R.mem);
     if (R.host) (void)hipHostFree(R.host);
+    if (R.xs) (void)hipStreamSynchronize(R.xs);
     if (R.ev) (void)hipEventDestroy(R.ev);
+    if (R.eva) (void)hipEventDestroy(R.eva);
+    if (R.evx) (void)hipEventDestroy(R.evx);
     if (R.s) (void)hipStreamDestroy(R.s);
+    if (R.xs) (void)hipStreamDestroy(R.xs);
     R = Rank();
 }
 
@@ -166,6 +173,9 @@ int setup_rank(const Part &p, int d, Rank &R)
     MCHK(hipSetDevice(R.dev));
     if (!R.s) MCHK(hipStreamCreateWithFlags(&R.s, hipStreamNonBlocking));
     if (!R.ev) MCHK(hipEventCreateWithFlags(&R.ev, hipEventDisableTiming));
+    if (!R.xs) MCHK(hipStreamCreateWithFlags(&R.xs, hipStreamNonBlocking));
+    if (!R.eva) MCHK(hipEventCreateWithFlags(&R.eva, hipEventDisableTiming));
+    if (!R.evx) MCHK(hipEventCreateWithFlags(&R.evx, hipEventDisableTiming));
     const long cs = p.NR * p.C, rs = p.rcount(d) * p.NC;
     const long mcount = p.M[d + 1] - p.M[d];
     const bool w1 = p.world == 1;
@@ -274,6 +284,50 @@ void *field_ptr(const Arr &a, int f, long off)
     return a.top + off;
 }
 
+// queue one copy of an exchange plan on stream `st` of its receiving rank
+int queue_copy(const std::vector<Rank> &rk, const mpfft_copy &c, hipStream_t st)
+{
+    const Rank &S = rk[c.src], &D = rk[c.dst];
+    const Arr &sa = c.src_layout ? S.row[c.op] : S.col[c.op];
+    const Arr &da = c.dst_layout ? D.row[c.op] : D.col[c.op];
+    const size_t es = c.field == 2 ? 4 : 8;
+    void *dp = field_ptr(da, c.field, c.dst_off);
+    const void *sp = field_ptr(sa, c.field, c.src_off);
+    if (dp == sp) return MPFFT_OK;   // world 1: the row layout is a view of the column layout
+    if (S.dev == D.dev) MCHK(hipMemcpyAsync(dp, sp, c.count * es, hipMemcpyDeviceToDevice, st));
+    else MCHK(hipMemcpyPeerAsync(dp, D.dev, sp, S.dev, c.count * es, st));
+    return MPFFT_OK;
+}
+
+// exchange #1 with the forward column passes run per operand: every receiver's exchange
+// stream pulls operand 1's blocks once all senders finished operand 1's passes (event eva)
+// -- while the compute streams run operand 2's passes -- then operand 2's (event ev); the
+// compute stream waits for both before the row passes
+int run_exchange_fwd(const Part &p, std::vector<Rank> &rk)
+{
+    std::vector<mpfft_copy> plan;
+    exchange_plan(p, MPFFT_XCHG_COL_TO_ROW, plan);
+    for (int d = 0; d < p.world; ++d) {
+        Rank &D = rk[d];
+        MCHK(hipSetDevice(D.dev));
+        for (int op = 0; op < 2; ++op) {
+            for (int s = 0; s < p.world; ++s) MCHK(hipStreamWaitEvent(D.xs, op ? rk[s].ev : rk[s].eva, 0));
+            for (const mpfft_copy &c : plan)
+                if (c.dst == d && c.op == op) {
+                    int rc = queue_copy(rk, c, D.xs);
+                    if (rc) return rc;
+                }
+        }
+        MCHK(hipEventRecord(D.evx, D.xs));
+    }
+    for (int d = 0; d < p.world; ++d) {   // senders' compute streams must not run ahead of the pulls
+        MCHK(hipSetDevice(rk[d].dev));
+        for (int s = 0; s < p.world; ++s) MCHK(hipStreamWaitEvent(rk[d].s, rk[s].evx, 0));
+        MCHK(hipEventRecord(rk[d].ev, rk[d].s));
+    }
+    return MPFFT_OK;
+}
+
 // queue one exchange: each receiver waits for every sender's last event, then pulls
 int run_exchange(const Part &p, std::vector<Rank> &rk, int which)
 {
@@ -285,15 +339,8 @@ int run_exchange(const Part &p, std::vector<Rank> &rk, int which)
             if (s != d) MCHK(hipStreamWaitEvent(rk[d].s, rk[s].ev, 0));
         for (const mpfft_copy &c : plan) {
             if (c.dst != d) continue;
-            const Rank &S = rk[c.src], &D = rk[c.dst];
-            const Arr &sa = c.src_layout ? S.row[c.op] : S.col[c.op];
-            const Arr &da = c.dst_layout ? D.row[c.op] : D.col[c.op];
-            const size_t es = c.field == 2 ? 4 : 8;
-            void *dp = field_ptr(da, c.field, c.dst_off);
-            const void *sp = field_ptr(sa, c.field, c.src_off);
-            if (dp == sp) continue;   // world 1: the row layout is a view of the column layout
-            if (S.dev == D.dev) MCHK(hipMemcpyAsync(dp, sp, c.count * es, hipMemcpyDeviceToDevice, D.s));
-            else MCHK(hipMemcpyPeerAsync(dp, D.dev, sp, S.dev, c.count * es, D.s));
+            int rc = queue_copy(rk, c, rk[d].s);
+            if (rc) return rc;
         }
     }
     for (int d = 0; d < p.world; ++d) {
@@ -303,7 +350,8 @@ int run_exchange(const Part &p, std::vector<Rank> &rk, int which)
     return MPFFT_OK;
 }
 
-int stage_all(const Part &p, std::vector<Rank> &rk, int stage, unsigned long depth, unsigned long w)
+int stage_all(const Part &p, std::vector<Rank> &rk, int stage, unsigned long depth, unsigned long w,
+              bool ev_a = false)
 {
     for (int d = 0; d < p.world; ++d) {
         Rank &R = rk[d];
@@ -315,7 +363,7 @@ int stage_all(const Part &p, std::vector<Rank> &rk, int stage, unsigned long dep
             std::swap(R.row[0], R.rowc);
             if (p.world == 1) std::swap(R.col[0], R.colc);
         }
-        MCHK(hipEventRecord(R.ev, R.s));
+        MCHK(hipEventRecord(ev_a ? R.eva : R.ev, R.s));
     }
     return MPFFT_OK;
 }
@@ -375,8 +423,9 @@ int mul_multi_locked(Ctx &X, uint64_t *r1, const uint64_t *i1, long n1, const ui
             if (trc[d]) return trc[d];
     }
 
-    if ((rc = stage_all(p, rk, MPFFT_SHARD_FWD_COLUMNS, depth, w))) return rc;
-    if ((rc = run_exchange(p, rk, MPFFT_XCHG_COL_TO_ROW))) return rc;
+    if ((rc = stage_all(p, rk, MPFFT_SHARD_FWD_COLUMNS_A, depth, w, true))) return rc;
+    if ((rc = stage_all(p, rk, MPFFT_SHARD_FWD_COLUMNS_B, depth, w))) return rc;
+    if ((rc = run_exchange_fwd(p, rk))) return rc;
     if ((rc = stage_all(p, rk, MPFFT_SHARD_FWD_ROWS, depth, w))) return rc;
     if ((rc = stage_all(p, rk, MPFFT_SHARD_POINTWISE, depth, w))) return rc;
     if ((rc = stage_all(p, rk, MPFFT_SHARD_INV_ROWS, depth, w))) return rc;

@@ -136,7 +136,9 @@ class ShardedMul:
     # point-to-point ops
     _FIELDS = ("dig", "cb", "top")
 
-    def _exchange(self, which):
+    def _exchange(self, which, op=None, wait=True):
+        """op: only that operand's copies; wait=False: returns the pending transfers
+        (comm.wait them later), so compute queued meanwhile overlaps the exchange."""
         p, me = self.p, self.rank
         W = p.world
 
@@ -144,7 +146,7 @@ class ShardedMul:
             return self.row[k] if layout else self.col[k]
         groups = {}
         for c in p.exchange_plan(which):
-            if me not in (c["src"], c["dst"]):
+            if me not in (c["src"], c["dst"]) or (op is not None and c["op"] != op):
                 continue
             f = self._FIELDS[c["field"]]
             send, recv = groups.setdefault((c["op"], c["field"]), ([None] * W, [None] * W))
@@ -157,7 +159,7 @@ class ShardedMul:
             send, recv = groups[(op, fi)]
             empty = self.col[op][self._FIELDS[fi]][:0]
             plan.append(([v if v is not None else empty for v in send], [v if v is not None else empty for v in recv]))
-        self.comm.exchange(plan)
+        return self.comm.exchange(plan, wait=wait)
 
     def run(self, i1, i2, mark=None):
         """i1, i2: this rank's operand column slices (ShardPlan.slice_operand; the full
@@ -165,9 +167,19 @@ class ShardedMul:
         mark(name), when given, is called after each phase (bench.py's per-phase events)."""
         p, be, sh = self.p, self.be, self.shard_desc()
         mark = mark or (lambda name: None)
-        be.stage("fwd_columns", sh, i1, i2)
-        mark("fwd_columns")
-        self._exchange(XCHG_COL_TO_ROW)
+        if getattr(be, "split_columns", False):
+            # operand 1's exchange in flight while operand 2's column passes run (on RCCL: the
+            # transfers go on the communicator's stream, queued behind operand 1's passes only)
+            be.stage("fwd_columns_a", sh, i1, i2)
+            pend = self._exchange(XCHG_COL_TO_ROW, op=0, wait=False)
+            be.stage("fwd_columns_b", sh, i1, i2)
+            mark("fwd_columns")
+            pend += self._exchange(XCHG_COL_TO_ROW, op=1, wait=False)
+            self.comm.wait(pend)
+        else:
+            be.stage("fwd_columns", sh, i1, i2)
+            mark("fwd_columns")
+            self._exchange(XCHG_COL_TO_ROW)
         mark("exchange1")
         be.stage("fwd_rows", sh, i1, i2)
         mark("fwd_rows")
@@ -233,9 +245,11 @@ class TorchComm:
         else:
             self.dist.all_to_all_single(out, inp, out_splits, in_splits)
 
-    def exchange(self, plan):
+    def exchange(self, plan, wait=True):
         """plan: [(send views by peer, recv views by peer)]; one batch of isend/irecv for
-        all of them (one RCCL group on GPUs), the rank's own views copied locally."""
+        all of them (one RCCL group on GPUs), the rank's own views copied locally.
+        wait=False (device buffers): returns the pending requests for wait(); host-staged
+        exchanges always complete here."""
         me = self.dist.get_rank()
         ops, back = [], []
         for send, recv in plan:
@@ -254,11 +268,18 @@ class TorchComm:
                     ops.append(self.dist.P2POp(self.dist.isend, sv.contiguous(), d))
                 if rv.numel():
                     ops.append(self.dist.P2POp(self.dist.irecv, rv, d))
-        if ops:
-            for r in self.dist.batch_isend_irecv(ops):
-                r.wait()
+        reqs = self.dist.batch_isend_irecv(ops) if ops else []
+        if wait or back:
+            self.wait(reqs)
+            reqs = []
         for dst, h in back:
             dst.copy_(h)
+        return reqs
+
+    @staticmethod
+    def wait(reqs):
+        for r in reqs:
+            r.wait()
 
     def all_gather(self, t):
         import torch
@@ -294,8 +315,11 @@ class GpuBackend:
     def _desc(self, sh):
         return self.mp.shard_desc(sh)
 
+    split_columns = True   # per-operand forward column stages (exchange #1 overlaps operand 2's)
+
     def stage(self, name, sh, i1, i2):
-        which = {"fwd_columns": 0, "fwd_rows": 1, "pointwise": 2, "inv_rows": 3, "inv_columns": 4}[name]
+        which = {"fwd_columns": 0, "fwd_rows": 1, "pointwise": 2, "inv_rows": 3, "inv_columns": 4,
+                 "fwd_columns_a": 5, "fwd_columns_b": 6}[name]
         self.mp.shard_stage(which, self._desc(sh), i1, i2, self.stream)
 
     def tail_coeffs(self, sh, H):
@@ -489,10 +513,15 @@ def bench(args, cfg_name, cfg, rank, world, dev):
 class _SoloComm:
     """world == 1: exchanges are local copies."""
 
-    def exchange(self, plan):
+    def exchange(self, plan, wait=True):
         for send, recv in plan:
             if not _same_view(recv[0], send[0]):
                 recv[0].copy_(send[0])
+        return []
+
+    @staticmethod
+    def wait(reqs):
+        pass
 
     def all_to_all(self, out, inp, out_splits, in_splits):
         out[: inp.numel()].copy_(inp)

@@ -65,11 +65,21 @@ class MockBackend:
     def stage(self, name, sh, i1, i2):
         getattr(self, "_" + name)(sh, i1, i2)
 
-    def _fwd_columns(self, sh, i1, i2):
+    split_columns = True   # per-operand forward column stages, as the GPU backend
+
+    def _fwd_columns_a(self, sh, i1, i2):
+        self._fwd_columns(sh, i1, i2, ops=(0,))
+
+    def _fwd_columns_b(self, sh, i1, i2):
+        self._fwd_columns(sh, i1, i2, ops=(1,))
+
+    def _fwd_columns(self, sh, i1, i2, ops=(0, 1)):
         p = self.p
         mask = (1 << p.bits1) - 1
         ch = sh.get("src_chunk", 0)
         for k, op in ((0, i1), (1, i2)):
+            if k not in ops:
+                continue
             X = int.from_bytes(op.numpy().view(np.uint64).tobytes(), "little")
             for cl in range(sh["ccount"]):
                 c = sh["c0"] + cl

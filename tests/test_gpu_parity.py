@@ -37,7 +37,8 @@ MFMA_SHAPES = [(9, 16, 2000, 1500), (8, 64, 3000, 2000), (7, 256, 4000, 3000), (
 # column / row passes, the twiddle-on-load first row pass, the general-multiplier last
 # inverse row pass, the fused split; truncation case a (T <= n) and b (T > n)
 BIG_SHAPES = [(8, 512, 40000, 40000), (8, 512, 140000, 140000), (8, 512, 100000, 30000),
-              (7, 2048, 150000, 120000), (9, 256, 120000, 200000)]
+              (7, 2048, 150000, 120000), (9, 256, 120000, 200000),
+              (7, 1024, 80000, 70000), (5, 4096, 20000, 19000)]   # l = 2048 case b: the doubled-column split
 
 
 @pytest.mark.parametrize("depth,w,n1,n2", STAGE_SHAPES + MFMA_SHAPES + BIG_SHAPES)
@@ -294,7 +295,9 @@ def test_fill_fold_l4096_case_b(mp, oracle, depth, w, nl):
 
 
 @pytest.mark.parametrize("depth,w,nl,alt", [(12, 32, 2200000, True), (13, 16, 4500000, True),
-                                            (14, 8, 9000000, True), (13, 16, 3000000, False)])
+                                            (14, 8, 9000000, True), (13, 16, 3000000, False),
+                                            (5, 4096, 20000, True), (6, 2048, 40000, True),
+                                            (7, 1024, 80000, True)])
 def test_mfa_split_l2048(mp, oracle, depth, w, nl, alt):
     """The plan's MFA split at l = 2048 (make_plan): truncation case b takes twice the
     reference's columns (mul_fft.c:3195) with four-level forward k_rpass passes (7 row or
@@ -317,7 +320,9 @@ def test_l4096_products_every_pointwise_kind(mp, oracle, kind):
     old = os.environ.get("MPFFT_POINTWISE")
     os.environ["MPFFT_POINTWISE"] = kind
     try:
-        for depth, w, n1, n2 in ((13, 32, 1000000, 999983), (17, 2, 1500000, 1400000)):
+        # + l = 2048 in truncation case b (the doubled-column split, four-level row passes: the
+        # canonical last row pass again falls back to k_bpass at its own level cap)
+        for depth, w, n1, n2 in ((13, 32, 1000000, 999983), (17, 2, 1500000, 1400000), (12, 32, 2200000, 2100000)):
             a = mp.fill_random(n1, 0x5005 + depth)
             b = mp.fill_random(n2, 0x6006 + w)
             assert (mp.mul(a, b, depth, w) == oracle.gmp_mul(a, b)).all(), (kind, depth, w)
