@@ -32,18 +32,35 @@
 // LDS of one k_pwss workgroup: M K limbs (the exchange rows, then the coefficients; the l
 // output overflows alias them) + tops + pending exponents.  C3 (M = 18, K = 256): 38 912 B,
 // so four workgroups share a CU's 160 KiB (pw_wpe).
+// Tight form (PW_TIGHT9, K = 512): no top / pending-exponent arrays beside the exchange rows --
+// a level's partner tops and exponents go by a wave shuffle (partner in the wave) or through
+// the first two exchange rows before the words are published (two more barriers), and the
+// signed coefficients are stored as two's complement (no sign array) -- so the workgroup needs
+// exactly M K 8 bytes: 80 KiB at C4 (M = 20), two workgroups per CU instead of one.
+#ifndef PW_TIGHT9
+#define PW_TIGHT9 1   // 0: the round-3 form (86 KB, one workgroup per CU at C4), for A/B builds
+#endif
+__host__ __device__ constexpr bool pw_tight(int K) { return PW_TIGHT9 && K == 512; }
+
 __host__ __device__ constexpr size_t pw_lds_bytes(int M, int K, int l)
 {
-    return ((size_t)M * K * 8 > (size_t)l * 4 ? (size_t)M * K * 8 : (size_t)l * 4) + (size_t)K * 8;
+    return ((size_t)M * K * 8 > (size_t)l * 4 ? (size_t)M * K * 8 : (size_t)l * 4) + (pw_tight(K) ? 0 : (size_t)K * 8);
 }
 
-// waves per SIMD k_pwss is compiled for: 4 (VGPRs <= 128) where four workgroups fit the LDS
-// (K = 256: 1024 threads per CU), else 2 (the compiler's choice, ~140-170 VGPRs)
+// waves per SIMD k_pwss is compiled for: 4 (VGPRs <= 128) where the LDS fits 1024 threads per
+// CU (K = 256: four workgroups; the tight K = 512 form: two), else 2 (the compiler's choice,
+// ~140-170 VGPRs)
 template <int M, int LK>
-__host__ __device__ constexpr int pw_wpe() { return LK == 8 && pw_lds_bytes(M, 1 << LK, 64 * M) * 4 <= 160 * 1024 ? 4 : 2; }
+__host__ __device__ constexpr int pw_wpe()
+{
+    return pw_lds_bytes(M, 1 << LK, 64 * M) * (1024 >> LK) <= 160 * 1024 ? 4 : 2;
+}
 // partner-word prefetch distance of pw_combine for that budget
+#ifndef PW_PD_TIGHT
+#define PW_PD_TIGHT 16
+#endif
 template <int M, int LK>
-__host__ __device__ constexpr int pw_pd() { return pw_wpe<M, LK>() == 4 ? 16 : 2 * M; }
+__host__ __device__ constexpr int pw_pd() { return pw_wpe<M, LK>() == 4 ? (pw_tight(1 << LK) ? PW_PD_TIGHT : 16) : 2 * M; }
 
 // Exchange format: thread t publishes its value as 2M 32-bit words, word k at
 // Xw[k K + t] (conflict-free for any rotation), top in TT[t].  Before publishing,
@@ -93,13 +110,14 @@ __host__ __device__ __forceinline__ int pw_norm(u64 (&L)[M], int T)
 //   negated (E >= N', or the signs differ):  ~out + 1 + (1 + T_q) 2^E'.
 // After pw_norm T_q = -1, so the (1 + T_q) term is a rare branch, and the whole sum is
 // one add-with-carry chain with carry-in 1.
+// packed: the partner's 2 T_q + S_q (TT[q], or a register in the tight form)
 template <int M, int LK, int PD = 2 * M>
 __host__ __device__ __forceinline__ void pw_combine(u64 (&L)[M], int &T, int &S, int alpha, const u32 *Xw,
-                                                   const int *TT, int q, unsigned E)
+                                                   int packed, int q, unsigned E)
 {
     constexpr int K = 1 << LK, NW = 2 * M;
     constexpr unsigned NP = 64 * M;
-    const int packed = TT[q], Tq = packed >> 1, Sq = packed & 1;
+    const int Tq = packed >> 1, Sq = packed & 1;
     bool neg = E >= NP;
     if (neg) E -= NP;
     const int Yw = ((int)E - 1) >> 5;                    // E = 0: Yw = -1, s5 = 32
@@ -310,18 +328,25 @@ __host__ __device__ __forceinline__ void pw_mulmod(u64 (&Z)[M], int &T, const u6
     T = (int)bw;   // value = Z + T 2^N', T in {-1, 0}
 }
 
-// exchange: thread t normalises its value (pw_norm) and publishes it as words + top
+// exchange: thread t publishes its value as words (normalised first: pw_norm) and, unless
+// TT is null (tight form), its top
 template <int M, int LK>
-__device__ __forceinline__ void pw_publish(u64 (&L)[M], int &T, int S, u32 *Xw, int *TT, int t)
+__device__ __forceinline__ void pw_publish_words(const u64 (&L)[M], u32 *Xw, int t)
 {
     constexpr int K = 1 << LK;
-    T = pw_norm<M>(L, T);
 #pragma unroll
     for (int j = 0; j < M; ++j) {
         Xw[(2 * j) * K + t] = (u32)L[j];
         Xw[(2 * j + 1) * K + t] = (u32)(L[j] >> 32);
     }
-    TT[t] = 2 * T + S;
+}
+
+template <int M, int LK>
+__device__ __forceinline__ void pw_publish(u64 (&L)[M], int &T, int S, u32 *Xw, int *TT, int t)
+{
+    T = pw_norm<M>(L, T);
+    pw_publish_words<M, LK>(L, Xw, t);
+    if (TT) TT[t] = 2 * T + S;
 }
 
 // One forward (DIF) or inverse (DIT) length-K cyclic transform with root 2^W2 over
@@ -359,21 +384,44 @@ __device__ __forceinline__ void pw_transform(u64 (&L)[M], int &T, int &S, unsign
         // (qt mod h) 2^j < K/2, times W2: below N' (= K W2 / 2): no reduction needed
         const unsigned tw = (unsigned)((qt & (h - 1)) << j) * W2;
         const bool cross = h >= 64;                  // partner in another wave
-        pw_publish<M, LK>(L, T, S, Xw, TT, t);
-        PP[t] = P;
-        if (cross) __syncthreads(); else pw_wave_sync();
-        const unsigned Pq = PP[q];
+        unsigned Pq;
+        int packed;
+        if (pw_tight(K)) {
+            // the partner's top / sign and exponent first (a shuffle, or through rows 0-1 before
+            // the words overwrite them), then the words
+            T = pw_norm<M>(L, T);
+            const int own = 2 * T + S;
+            if (cross) {
+                Xw[t] = (u32)own;
+                Xw[K + t] = P;
+                __syncthreads();
+                packed = (int)Xw[q];
+                Pq = Xw[K + q];
+                __syncthreads();
+            } else {
+                packed = __shfl_xor(own, h);
+                Pq = (unsigned)__shfl_xor((int)P, h);
+            }
+            pw_publish_words<M, LK>(L, Xw, t);
+            if (cross) __syncthreads(); else pw_wave_sync();
+        } else {
+            pw_publish<M, LK>(L, T, S, Xw, TT, t);
+            PP[t] = P;
+            if (cross) __syncthreads(); else pw_wave_sync();
+            Pq = PP[q];
+            packed = TT[q];
+        }
         unsigned E;
         if (DIR == 0) {
             // top: X_t + X_q = 2^P (x_t + 2^(Pq-P) x_q); bottom: (X_q - X_t) w^tw = 2^(P+tw) (2^(Pq-P) x_q - x_t)
             E = pw_mod(Pq + N2 - P, N2);
-            pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, top ? 1 : -1, Xw, TT, q, E);
+            pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, top ? 1 : -1, Xw, packed, q, E);
             if (!top) P = pw_mod(P + tw, N2);
         } else {
             // top: Z_t + Z_q w^-tw = 2^P (z_t + 2^(Pq-tw-P) z_q)
             // bottom: Z_q - Z_t w^-tw = 2^(P-tw) (2^(Pq-P+tw) z_q - z_t)
             E = top ? pw_mod(Pq + 2 * N2 - tw - P, N2) : pw_mod(Pq + N2 - P + tw, N2);
-            pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, top ? 1 : -1, Xw, TT, q, E);
+            pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, top ? 1 : -1, Xw, packed, q, E);
             if (!top) P = pw_mod(P + N2 - tw, N2);
         }
         if (cross) __syncthreads(); else pw_wave_sync();
@@ -551,17 +599,28 @@ __device__ __forceinline__ void pw_slot_product(u64 (&La)[M], int Ta, u64 (&Lb)[
         const unsigned un = (((unsigned)t * W2) >> 1) + lk + (half ? 1 : 0);   // < N' + lk + 1
         const unsigned F = pw_mod(Pz + N2 - un + (half ? NP / 4 : 0), N2);
         if (half) pw_sqrt2<M>(Z, Tz);
-        pw_publish<M, LK>(Z, Tz, Sz, Xw, TT, t);
+        pw_publish<M, LK>(Z, Tz, Sz, Xw, pw_tight(K) ? nullptr : TT, t);
         pw_wave_sync();                                  // own column only
-        pw_combine<M, LK, pw_pd<M, LK>()>(Z, Tz, Sz, 0, Xw, TT, t, F);   // clears the sign flag
+        pw_combine<M, LK, pw_pd<M, LK>()>(Z, Tz, Sz, 0, Xw, 2 * Tz + Sz, t, F);   // clears the sign flag
         __syncthreads();                                 // the u64 rows below cross columns
     }
     // signed coefficient c_t = v - s p', v in [0, 2^N'], s = (v > 2^(N'-1))
     const int zt = pw_canon<M>(Z, Tz);
     const int neg = zt || (Z[M - 1] >> 63);
+    if (pw_tight(K)) {
+        // as N'-bit two's complement: v - s (v - 1 = 2^N' - 1 for v = 2^N'), its top bit the sign
+        u64 b = (u64)neg;
 #pragma unroll
-    for (int j = 0; j < M; ++j) X[j * K + t] = Z[j];
-    TT[t] = neg | (zt << 1);                     // s, and limb M of v (2^N' only)
+        for (int j = 0; j < M; ++j) {
+            const u64 z = Z[j];
+            X[j * K + t] = z - b;
+            b = b && z == 0;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < M; ++j) X[j * K + t] = Z[j];
+        TT[t] = neg | (zt << 1);                     // s, and limb M of v (2^N' only)
+    }
     __syncthreads();
     PW_STAMP(6);
 #undef PW_STAMP
@@ -598,9 +657,14 @@ __device__ __forceinline__ void pw_slot_output(const u64 *X, const int *TT, int 
             if (hi > K - 1) hi = K - 1;
             for (int tp = lo; tp <= hi; ++tp) {
                 const int d = mm - tp * LP;        // limb of c_tp, 0 .. M
-                const int tt = TT[tp];
-                i128 v = d < M ? (i128)X[(size_t)d * K + tp] : (i128)(tt >> 1);
-                if ((tt & 1) && (d == 0 || d == M)) v -= 1;
+                i128 v;
+                if (pw_tight(K)) {                 // two's complement: limb M is the sign extension
+                    v = d < M ? (i128)X[(size_t)d * K + tp] : -(i128)(X[(size_t)(M - 1) * K + tp] >> 63);
+                } else {
+                    const int tt = TT[tp];
+                    v = d < M ? (i128)X[(size_t)d * K + tp] : (i128)(tt >> 1);
+                    if ((tt & 1) && (d == 0 || d == M)) v -= 1;
+                }
                 S += wrap ? -v : v;
             }
         }
@@ -655,8 +719,8 @@ __global__ __launch_bounds__(1 << LK) __attribute__((amdgpu_waves_per_eu(pw_wpe<
     const int t = threadIdx.x;
     u64 *X = (u64 *)smem;                        // M K limbs (2M word rows during the transforms)
     u32 *Xw = (u32 *)smem;
-    int *TT = (int *)(X + (size_t)M * K);        // K
-    unsigned *PP = (unsigned *)(TT + K);         // K
+    int *TT = pw_tight(K) ? nullptr : (int *)(X + (size_t)M * K);    // K (none in the tight form)
+    unsigned *PP = pw_tight(K) ? nullptr : (unsigned *)(TT + K);     // K
     int *H = (int *)smem;                        // l, over X (pw_slot_output)
     const int cbw = cb_words(l);
     constexpr int CLP = pw_piece_limbs<M, LK>();   // == l / K (host: pw_inner_limbs)

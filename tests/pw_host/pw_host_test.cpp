@@ -37,7 +37,7 @@ template <int M> int run() {
         // represented values carry a sign flag: (-1)^S (L + T 2^N')
         tovals<M>(a, L, T); if (S) mpz_neg(a, a); if (Sq) mpz_neg(b, b);
         mpz_ui_pow_ui(e2, 2, E); mpz_mul(want, b, e2); mpz_mul_si(a, a, alpha); mpz_add(want, want, a); mpz_mod(want, want, p);
-        pw_combine<M, LK>(L, T, S, alpha, Xw, TT, q, E);
+        pw_combine<M, LK>(L, T, S, alpha, Xw, TT[q], q, E);
         tovals<M>(got, L, T); if (S) mpz_neg(got, got); mpz_mod(got, got, p);
         if (mpz_cmp(got, want)) { if (bad++ < 5) printf("combine mismatch it=%d E=%u alpha=%d Tq=%d\n", it, E, alpha, Tq); }
     }
