@@ -27,6 +27,7 @@
 // The coefficients are then summed (with their signs and the negacyclic wrap) into
 // the l output limbs and stored in the reduced HBM form the inverse pass loads.
 #pragma once
+#include <type_traits>
 #include "coeff.hpp"
 
 // LDS of one k_pwss workgroup: M K limbs (the exchange rows, then the coefficients; the l
@@ -41,6 +42,11 @@
 #define PW_TIGHT9 1   // 0: the round-3 form (86 KB, one workgroup per CU at C4), for A/B builds
 #endif
 __host__ __device__ constexpr bool pw_tight(int K) { return PW_TIGHT9 && K == 512; }
+// operand B's pieces loaded after A's forward transform (pw_slot_product's loadB)
+#ifndef PW_LATE_B_ALL
+#define PW_LATE_B_ALL 0
+#endif
+__host__ __device__ constexpr bool pw_late_b(int K) { return pw_tight(K) || PW_LATE_B_ALL; }
 
 __host__ __device__ constexpr size_t pw_lds_bytes(int M, int K, int l)
 {
@@ -558,10 +564,14 @@ __device__ __forceinline__ void pw_load_pair_bfly(u64 (&L)[M], int &T, const u64
 // inner product of one slot: forward transforms of the pieces (La, Ta), (Lb, Tb), the
 // pointwise products in R', the inverse and the un-weighting; leaves the signed
 // coefficients c_t in X (limb-major, M rows) and their signs (+ limb M) in TT (ends with a barrier)
-template <int M, int LK>
+// loadB(Lb, Tb): when given (the tight form), operand B's pieces are loaded only after A's
+// forward transform, so the two operands' raw and formed pieces are never live together (the
+// kernel's register peak at 128 VGPRs; B's load latency is hidden by the CU's other workgroup)
+template <int M, int LK, typename LoadB = int>
 __device__ __forceinline__ void pw_slot_product(u64 (&La)[M], int Ta, u64 (&Lb)[M], int Tb, u64 *X, u32 *Xw, int *TT,
-                                                unsigned *PP, int t, unsigned long long *stamp)
+                                                unsigned *PP, int t, unsigned long long *stamp, LoadB loadB = 0)
 {
+    constexpr bool late_b = !std::is_same<LoadB, int>::value;
 #define PW_STAMP(k) do { if (stamp && t == 0) stamp[k] = __builtin_amdgcn_s_memtime(); } while (0)
     constexpr int K = 1 << LK, lk = LK;
     constexpr unsigned NP = 64 * M, N2 = 2 * NP;
@@ -574,11 +584,15 @@ __device__ __forceinline__ void pw_slot_product(u64 (&La)[M], int Ta, u64 (&Lb)[
     unsigned Pa = (((unsigned)t * W2) >> 1) + (half ? NP / 4 : 0), Pb = Pa;   // < N' + N'/4
     if (half) {
         pw_sqrt2<M>(La, Ta);
-        pw_sqrt2<M>(Lb, Tb);
+        if (!late_b) pw_sqrt2<M>(Lb, Tb);
     }
     PW_STAMP(1);
     pw_transform<M, LK, 0>(La, Ta, Sa, Pa, Xw, TT, PP, W2, t);
     PW_STAMP(2);
+    if constexpr (late_b) {
+        loadB(Lb, Tb);
+        if (half) pw_sqrt2<M>(Lb, Tb);
+    }
     pw_transform<M, LK, 0>(Lb, Tb, Sb, Pb, Xw, TT, PP, W2, t);
     PW_STAMP(3);
 
@@ -725,8 +739,18 @@ __global__ __launch_bounds__(1 << LK) __attribute__((amdgpu_waves_per_eu(pw_wpe<
     const int cbw = cb_words(l);
     constexpr int CLP = pw_piece_limbs<M, LK>();   // == l / K (host: pw_inner_limbs)
     u64 La[M], Lb[M];
-    int Ta, Tb;
-    if (FUSE == 0) {
+    int Ta = 0, Tb = 0;
+    if (FUSE == 0 && pw_late_b(K)) {
+        const long slot = blockIdx.x;
+        pw_load_piece<M, CLP>(La, Ta, digA + (size_t)slot * l, cbA + (size_t)slot * cbw, topA + slot, l, t);
+        auto loadB = [&](u64 (&L)[M], int &T) {
+            pw_load_piece<M, CLP>(L, T, digB + (size_t)slot * l, cbB + (size_t)slot * cbw, topB + slot, l, t);
+        };
+        pw_slot_product<M, LK>(La, Ta, Lb, Tb, X, Xw, TT, PP, t, stamp, loadB);
+        // every piece of A was read before the first barrier of A's transform: the output may
+        // overwrite A in place
+        pw_slot_output<M, LK>(X, TT, H, digA + (size_t)slot * l, cbA + (size_t)slot * cbw, topA + slot, l, t);
+    } else if (FUSE == 0) {
         const long slot = blockIdx.x;
         {
             PwRaw<CLP> RA, RB;   // both operands' bytes requested before either is used
@@ -749,8 +773,15 @@ __global__ __launch_bounds__(1 << LK) __attribute__((amdgpu_waves_per_eu(pw_wpe<
             slot = 2 * (((j >> 1) << 3) + x) + (j & 1);
         }
         pw_load_pair_bfly<M, CLP>(La, Ta, digA, cbA, topA, slot & ~1L, l, cbw, t, slot & 1);
-        pw_load_pair_bfly<M, CLP>(Lb, Tb, digB, cbB, topB, slot & ~1L, l, cbw, t, slot & 1);
-        pw_slot_product<M, LK>(La, Ta, Lb, Tb, X, Xw, TT, PP, t, stamp);
+        if (pw_late_b(K)) {
+            auto loadB = [&](u64 (&L)[M], int &T) {
+                pw_load_pair_bfly<M, CLP>(L, T, digB, cbB, topB, slot & ~1L, l, cbw, t, slot & 1);
+            };
+            pw_slot_product<M, LK>(La, Ta, Lb, Tb, X, Xw, TT, PP, t, stamp, loadB);
+        } else {
+            pw_load_pair_bfly<M, CLP>(Lb, Tb, digB, cbB, topB, slot & ~1L, l, cbw, t, slot & 1);
+            pw_slot_product<M, LK>(La, Ta, Lb, Tb, X, Xw, TT, PP, t, stamp);
+        }
         pw_slot_output<M, LK>(X, TT, H, digC + (size_t)slot * l, cbC + (size_t)slot * cbw, topC + slot, l, t);
     }
     if (stamp) {
