@@ -42,11 +42,10 @@
 #define PW_TIGHT9 1   // 0: the round-3 form (86 KB, one workgroup per CU at C4), for A/B builds
 #endif
 __host__ __device__ constexpr bool pw_tight(int K) { return PW_TIGHT9 && K == 512; }
-// operand B's pieces loaded after A's forward transform (pw_slot_product's loadB)
-#ifndef PW_LATE_B_ALL
-#define PW_LATE_B_ALL 0
-#endif
-__host__ __device__ constexpr bool pw_late_b(int K) { return pw_tight(K) || PW_LATE_B_ALL; }
+// operand B's pieces loaded after A's forward transform (pw_slot_product's loadB): the tight
+// form only (C4 pointwise 39.0 -> 37.7 ms; at l = 2048, four workgroups per CU, 0.5-2 % slower:
+// profiles/r04/pw_tight_ab.txt)
+__host__ __device__ constexpr bool pw_late_b(int K) { return pw_tight(K); }
 
 __host__ __device__ constexpr size_t pw_lds_bytes(int M, int K, int l)
 {
