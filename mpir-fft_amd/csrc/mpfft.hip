@@ -89,6 +89,7 @@ struct Plan {
     // (Exec::zflags) -- no stage between that pass and the combine may use this region
     size_t off_digA, off_topA, off_cbA, off_digB, off_topB, off_cbB, off_flags, bytes;
     bool has_c;         // a third coefficient array C: the fused pointwise (k_pwss PAIR) writes there
+    int fuse_rows;      // row DIF levels that run inside the pointwise: 1 (slot pairs), 2 (slot quads), 0
     size_t off_digC, off_topC, off_cbC;
 };
 
@@ -124,11 +125,12 @@ static int pwss_lk_of(long l)
     return 0;
 }
 
-// the fused-pair k_pwss instance (last row DIF level on load, product to C) exists for l
-static bool pw_pair_kernel(long l)
+// the fused-pair k_pwss instance (last row DIF level on load, product to C) exists for l;
+// fuse 2: the fused-quad instance (the last two levels)
+static bool pw_pair_kernel(long l, int fuse = 1)
 {
     const int lk = pwss_lk_of(l);
-    return lk && pw_get(pw_inner_limbs(l, lk), lk, 1) != nullptr;
+    return lk && pw_get(pw_inner_limbs(l, lk), lk, fuse) != nullptr;
 }
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -235,9 +237,19 @@ static int make_plan_split(Plan *p, long n1, long n2, unsigned long depth, unsig
     // C: output of the fused last-row-level pointwise (single-GPU new_mpn_mul, Exec::row_fused)
     // (only where it saves a row pass: fewer passes for lbC - 1 levels than for lbC)
     {
+        // the last two levels where that saves a pass and one does not (C4: 8 row levels at <= 3
+        // per pass are 3 + 3 + 2, 6 are 3 + 3); the quad form needs the plain MFA row root (not
+        // the sqrt2 front end's)
         const int ml = p->maxlogg > 0 ? p->maxlogg : 1;
-        const bool saves = (p->lbC - 1 + ml - 1) / ml < (p->lbC + ml - 1) / ml;
-        p->has_c = p->lbC >= 2 && saves && pw_pair_kernel(p->l);
+        auto np = [&](int L) { return (L + ml - 1) / ml; };
+        const bool f1 = p->lbC >= 2 && np(p->lbC - 1) < np(p->lbC) && pw_pair_kernel(p->l);
+        static const bool no2 = diag_env("MPFFT_NO_FUSE2") != nullptr;   // diagnostics: A/B
+        const int lk = pwss_lk_of(p->l);   // quad inputs are 4x the pieces: 2 more bits of headroom (pdispatch.hpp)
+        const bool room = lk && 64 * pw_inner_limbs(p->l, lk) >= 2 * ((64 * p->l) >> lk) + lk + 6;
+        const bool f2 = !sqrt2 && !no2 && room && p->lbC >= 3 && np(p->lbC - 2) < np(p->lbC - 1) &&
+                        np(p->lbC - 2) < np(p->lbC) && pw_pair_kernel(p->l, 2);
+        p->fuse_rows = f2 ? 2 : f1 ? 1 : 0;
+        p->has_c = p->fuse_rows > 0;
     }
     if (p->has_c) {
         p->off_digC = o; o += dig;
@@ -698,13 +710,15 @@ struct Exec {
     // the last row level fused into k_pwss: slot pairs (2i, 2i + 1) of a row adjacent (any row
     // layout with column blocks of ccb >= 2), a nested negacyclic pointwise with its fused-pair
     // instance, and a row pass left to apply the MFA twiddle
-    bool row_fused() const
+    // row DIF levels fused into the pointwise (0, 1 or 2)
+    int row_fused() const
     {
         static const bool off = [] { const char *e = diag_env("MPFFT_FUSE_ROW"); return e && !strcmp(e, "0"); }();
-        return fuse_row_last && !off && P.has_c && cview.dig[0] && pw_pair_kernel(P.l) && ccb >= 2;
+        const int f = P.fuse_rows;
+        return fuse_row_last && !off && f && cview.dig[0] && pw_pair_kernel(P.l, f) && ccb >= (1 << f) ? f : 0;
     }
 
-    int row_levels() const { return P.lbC - (row_fused() ? 1 : 0); }
+    int row_levels() const { return P.lbC - row_fused(); }
 
     PassArgs row_pass_args(int lvl, int k, int L) const
     {
@@ -761,8 +775,9 @@ struct Exec {
         if (cnt == 0) return MPFFT_OK;
         if (const int lk = pwss_lk(P.l)) {
             const int M = pw_inner_limbs(P.l, lk);
-            const bool pair = row_fused();
-            pw_fn f = pw_get(M, lk, pair ? 1 : 0);
+            const int fz = row_fused();
+            const bool pair = fz > 0;
+            pw_fn f = pw_get(M, lk, fz);
             if (f) {
                 const size_t lds = pw_lds(M, 1 << lk, (int)P.l);
                 allow_lds((const void *)f, lds);
@@ -1304,7 +1319,7 @@ static int run_all6(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, u
     if ((rc = X1.fwd_rows(2))) return rc;
     if (two && (rc = X2.fwd_rows(2))) return rc;
     pc.mark(2, s);
-    const bool fused = X1.row_fused();
+    const bool fused = X1.row_fused() > 0;
     if ((rc = X1.pointwise())) return rc;
     if (two && (rc = X2.pointwise())) return rc;
     pc.mark(3, s);
@@ -1391,14 +1406,14 @@ int mpfft_stage_kernels(long n1, long n2, unsigned long depth, unsigned long w, 
     int rc = make_plan(&P, n1, n2, depth, w);
     if (rc) return rc;
     const char *pass = P.big ? (P.rpass ? "k_rpass" : "k_bpass") : (P.wave && P.lds) ? "k_lpass" : P.wave ? "k_wpass" : "k_pass";
-    char pw[64];
+    char pw[96];
     const int lk = Exec::pwss_lk(P.l);
     const char *rows = P.big && P.rpass && !(lk && pw_get(pw_inner_limbs(P.l, lk), lk)) ? "k_rpass + k_bpass (canonical last pass)" : pass;
     const char *fz = diag_env("MPFFT_FUSE_ROW");
     const bool fused = P.has_c && !(fz && !strcmp(fz, "0"));   // as Exec::row_fused() in run_all
     if (lk && pw_get(pw_inner_limbs(P.l, lk), lk))
         snprintf(pw, sizeof pw, "k_pwss<%d>%s (nested negacyclic, K=%d)", pw_inner_limbs(P.l, lk),
-                 fused ? " pair + last row level" : "", 1 << lk);
+                 !fused ? "" : P.fuse_rows == 2 ? " quad + last two row levels" : " pair + last row level", 1 << lk);
     else if (P.l % 256 == 0 && P.l <= 4096 && pw_kind() != PW_MFMA1 && pw_kind() != PW_VALU)
         snprintf(pw, sizeof pw, "k_pwm2 (int8 MFMA)");
     else if (P.l % 128 == 0 && pw_kind() != PW_VALU)
@@ -1582,7 +1597,7 @@ int mpfft_shard_row_fused(long n1, long n2, unsigned long depth, unsigned long w
 {
     Plan P;
     if (make_plan(&P, n1, n2, depth, w)) return 0;
-    return P.has_c && pw_pair_kernel(P.l) && ccb >= 2 && !(P.NC % ccb);
+    return P.has_c && pw_pair_kernel(P.l, P.fuse_rows) && ccb >= (1 << P.fuse_rows) && !(P.NC % ccb);
 }
 
 int mpfft_shard_stage(int stage, const mpfft_shard *sh, const uint64_t *d_i1, const uint64_t *d_i2, void *stream)

@@ -560,6 +560,58 @@ __device__ __forceinline__ void pw_load_pair_bfly(u64 (&L)[M], int &T, const u64
     (void)Tb;
 }
 
+// Piece t of output pos (0..3) of the row DIF's last two levels on the slot quad x0..x3
+// (positions 4i..4i+3 of a row, the levels h = 2 and h = 1 of a length-NC DIF with root
+// 2^(w NR)): z0 = (x0 + x2) + (x1 + x3), z1 = (x0 + x2) - (x1 + x3), z2 = (x0 - x2) + w (x1 - x3),
+// z3 = (x0 - x2) - w (x1 - x3), with w = 2^(w NR NC / 4) = 2^(N/2): piece t of 2^(N/2) v is
+// piece t ^ K/2 of v, negated for t < K/2 (2^N == -1) -- a load address, not arithmetic.
+// Linear, so the pieces of z are signed sums of the inputs' pieces (|c_t| grows 4x: the inner
+// ring's headroom covers it, pdispatch.hpp).  Sums are kept in LP + 1 limbs two's complement,
+// one input piece formed at a time (registers), then sign-extended to M limbs.
+template <int M, int LP, int K>
+__device__ __forceinline__ void pw_load_quad_bfly(u64 (&L)[M], int &T, const u64 *dig, const u64 *cb, const int *top,
+                                                  long s0, int pos, int l, int cbw, int t)
+{
+    u64 acc[LP + 1];
+#pragma unroll
+    for (int j = 0; j <= LP; ++j) acc[j] = 0;
+    const int tr = t ^ (K / 2), sg = t >= K / 2 ? 1 : -1;
+    // sign of input slot q in output pos; x1, x3 come from the rotated piece for pos >= 2
+    auto sign_of = [&](int q) {
+        return q == 0 ? 1 : q == 2 ? (pos < 2 ? 1 : -1)
+             : (pos < 2 ? (pos == 0 ? 1 : -1) : (pos == 2 ? sg : -sg) * (q == 1 ? 1 : -1));
+    };
+    auto add = [&](const PwRaw<LP> &R, int q, int pt) {
+        u64 X[M];
+        int Tx;
+        pw_piece_make<M, LP>(X, Tx, R, l, pt);
+        // acc += sign * (limbs 0 .. LP of X): limb LP of X is the piece's carry, sign-extended
+        const u32 m = sign_of(q) < 0 ? ~0u : 0u;
+        u32 c = m & 1u;
+#pragma unroll
+        for (int j = 0; j <= LP; ++j) {
+            const u32 lo = __builtin_addc((u32)acc[j], (u32)X[j] ^ m, c, &c);
+            const u32 hi = __builtin_addc((u32)(acc[j] >> 32), (u32)(X[j] >> 32) ^ m, c, &c);
+            acc[j] = ((u64)hi << 32) | lo;
+        }
+    };
+    // two inputs' bytes in flight at a time (x0, x2 at piece t; then x1, x3)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int qa = h, qb = h + 2, pt = h && pos >= 2 ? tr : t;
+        PwRaw<LP> Ra, Rb;
+        pw_piece_fetch<LP>(Ra, dig + (size_t)(s0 + qa) * l, cb + (size_t)(s0 + qa) * cbw, top + s0 + qa, l, pt);
+        pw_piece_fetch<LP>(Rb, dig + (size_t)(s0 + qb) * l, cb + (size_t)(s0 + qb) * cbw, top + s0 + qb, l, pt);
+        add(Ra, qa, pt);
+        add(Rb, qb, pt);
+    }
+    // |sum| < 2^(64 LP + 3): limb LP's sign is the value's sign
+    const u64 up = (i64)acc[LP] < 0 ? ~0ull : 0ull;
+#pragma unroll
+    for (int j = 0; j < M; ++j) L[j] = j <= LP ? acc[j] : up;
+    T = (i64)acc[LP] < 0 ? -1 : 0;
+}
+
 // inner product of one slot: forward transforms of the pieces (La, Ta), (Lb, Tb), the
 // pointwise products in R', the inverse and the un-weighting; leaves the signed
 // coefficients c_t in X (limb-major, M rows) and their signs (+ limb M) in TT (ends with a barrier)
@@ -761,6 +813,27 @@ __global__ __launch_bounds__(1 << LK) __attribute__((amdgpu_waves_per_eu(pw_wpe<
         __syncthreads();   // every piece read before any output limb is written (in place on A)
         pw_slot_product<M, LK>(La, Ta, Lb, Tb, X, Xw, TT, PP, t, stamp);
         pw_slot_output<M, LK>(X, TT, H, digA + (size_t)slot * l, cbA + (size_t)slot * cbw, topA + slot, l, t);
+    } else if (FUSE == 2) {
+        // the row DIF's last two levels on load, slot quads: blocks b, b + 8, b + 16, b + 24 take
+        // the four slots of one quad, so they run on one XCD and share its L2 (identity on the
+        // tail of < 32 blocks)
+        const long b = blockIdx.x, nb = gridDim.x, main = nb - nb % 32;
+        long slot = b;
+        if (b < main) {
+            const long x = b & 7, j = b >> 3;
+            slot = 4 * (((j >> 2) << 3) + x) + (j & 3);
+        }
+        const long s0 = slot & ~3L;
+        const int pos = (int)(slot & 3);
+        pw_load_quad_bfly<M, CLP, K>(La, Ta, digA, cbA, topA, s0, pos, l, cbw, t);
+        if (pw_late_b(K)) {
+            auto loadB = [&](u64 (&L)[M], int &T) { pw_load_quad_bfly<M, CLP, K>(L, T, digB, cbB, topB, s0, pos, l, cbw, t); };
+            pw_slot_product<M, LK>(La, Ta, Lb, Tb, X, Xw, TT, PP, t, stamp, loadB);
+        } else {
+            pw_load_quad_bfly<M, CLP, K>(Lb, Tb, digB, cbB, topB, s0, pos, l, cbw, t);
+            pw_slot_product<M, LK>(La, Ta, Lb, Tb, X, Xw, TT, PP, t, stamp);
+        }
+        pw_slot_output<M, LK>(X, TT, H, digC + (size_t)slot * l, cbC + (size_t)slot * cbw, topC + slot, l, t);
     } else {
         // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs (blockIdx mod 8), each
         // with its own L2.  Blocks b and b + 8 take the two slots of one pair, so the second

@@ -4,9 +4,9 @@
 
 pw_fn pw_get(int M, int lk, int fuse)
 {
-    if (M == 10 && lk == 8) return fuse ? k_pwss<10, 8, 1> : k_pwss<10, 8, 0>;   // l = 1024
-    if (M == 18 && lk == 8) return fuse ? k_pwss<18, 8, 1> : k_pwss<18, 8, 0>;   // l = 2048
-    if (M == 20 && lk == 9) return fuse ? k_pwss<20, 9, 1> : k_pwss<20, 9, 0>;   // l = 4096
+    if (M == 10 && lk == 8) return fuse == 2 ? nullptr : fuse ? k_pwss<10, 8, 1> : k_pwss<10, 8, 0>;   // l = 1024
+    if (M == 18 && lk == 8) return fuse == 2 ? k_pwss<18, 8, 2> : fuse ? k_pwss<18, 8, 1> : k_pwss<18, 8, 0>;   // l = 2048
+    if (M == 20 && lk == 9) return fuse == 2 ? k_pwss<20, 9, 2> : fuse ? k_pwss<20, 9, 1> : k_pwss<20, 9, 0>;   // l = 4096
     return nullptr;
 }
 

@@ -310,6 +310,17 @@ def test_mfa_split_l2048(mp, oracle, depth, w, nl, alt):
     assert (mp.mul(a, b, depth, w) == oracle.gmp_mul(a, b)).all()
 
 
+@pytest.mark.parametrize("depth,w,n1,n2", [(16, 4, 3000000, 2999991), (17, 2, 1500000, 1400000)])
+def test_quad_fused_rows(mp, oracle, depth, w, n1, n2):
+    """The row DIF's last two levels inside the pointwise (k_pwss FUSE 2: slot quads, the h = 2
+    level's twiddle 2^(N/2) as a piece rotation on load) where that saves a row pass (l = 4096,
+    8 row levels: 3 + 3 instead of 3 + 3 + 2, C4's shape); whole products against GMP."""
+    assert "quad + last two row levels" in mp.stage_kernels(n1, n2, depth, w)["pointwise"]
+    a = mp.fill_random(n1, 0xB00B + depth)
+    b = mp.fill_random(n2, 0xC00C + w)
+    assert (mp.mul(a, b, depth, w) == oracle.gmp_mul(a, b)).all()
+
+
 @pytest.mark.parametrize("kind", ["mfma", "mfma1", "valu"])
 def test_l4096_products_every_pointwise_kind(mp, oracle, kind):
     """Whole products at l = 4096 with every MPFFT_POINTWISE family.  Those kinds need the
