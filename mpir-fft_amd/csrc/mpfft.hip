@@ -246,9 +246,15 @@ static int make_plan_split(Plan *p, long n1, long n2, unsigned long depth, unsig
         static const bool no2 = diag_env("MPFFT_NO_FUSE2") != nullptr;   // diagnostics: A/B
         const int lk = pwss_lk_of(p->l);   // quad inputs are 4x the pieces: 2 more bits of headroom (pdispatch.hpp)
         const bool room = lk && 64 * pw_inner_limbs(p->l, lk) >= 2 * ((64 * p->l) >> lk) + lk + 6;
-        const bool f2 = !sqrt2 && !no2 && room && p->lbC >= 3 && np(p->lbC - 2) < np(p->lbC - 1) &&
-                        np(p->lbC - 2) < np(p->lbC) && pw_pair_kernel(p->l, 2);
-        p->fuse_rows = f2 ? 2 : f1 ? 1 : 0;
+        // ... or where it turns four-level row passes into three-level ones (8 row levels: 4 + 4 ->
+        // fused 2 + 3 + 3 -- three-level passes run two workgroups per CU; C3 8.64 -> 8.55 ms,
+        // profiles/r04/quad_fuse_ab.txt)
+        const bool saves2 = np(p->lbC - 2) < np(p->lbC - 1) && np(p->lbC - 2) < np(p->lbC);
+        const bool to3 = ml == 4 && p->lbC - 2 == 6;
+        const bool f2 = !sqrt2 && !no2 && room && p->lbC >= 3 && (saves2 || to3) && pw_pair_kernel(p->l, 2);
+        static const bool force2 = diag_env("MPFFT_FORCE_FUSE2") != nullptr;   // diagnostics: A/B
+        const bool f2f = force2 && !sqrt2 && room && p->lbC >= 3 && pw_pair_kernel(p->l, 2);
+        p->fuse_rows = (f2 || f2f) ? 2 : f1 ? 1 : 0;
         p->has_c = p->fuse_rows > 0;
     }
     if (p->has_c) {
