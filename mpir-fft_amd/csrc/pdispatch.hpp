@@ -7,7 +7,9 @@ typedef void (*pw_fn)(uint64_t *, uint64_t *, int *, const uint64_t *, const uin
                       uint64_t *, uint64_t *, int *, unsigned long long *);
 
 // k_pwss<M, lk, fuse> (M = inner coefficient limbs, 2^lk pieces; fuse 1: the row DIF's last
-// level fused into the load, product to the C arrays), nullptr if not built
+// level fused into the load, product to the C arrays; fuse 2: the last two levels, slot quads
+// -- their pieces are 4x the inputs', so the plan checks 64 M >= 2 B + lk + 6), nullptr if
+// not built
 pw_fn pw_get(int M, int lk, int fuse = 0);
 size_t pw_lds(int M, int K, int l);
 

@@ -45,7 +45,13 @@ __host__ __device__ constexpr bool pw_tight(int K) { return PW_TIGHT9 && K == 51
 // operand B's pieces loaded after A's forward transform (pw_slot_product's loadB): the tight
 // form only (C4 pointwise 39.0 -> 37.7 ms; at l = 2048, four workgroups per CU, 0.5-2 % slower:
 // profiles/r04/pw_tight_ab.txt)
-__host__ __device__ constexpr bool pw_late_b(int K) { return pw_tight(K); }
+#ifndef PW_LATE_B_ALL
+#define PW_LATE_B_ALL 0   // A/B builds: the late operand-B load at every size
+#endif
+__host__ __device__ constexpr bool pw_late_b(int K) { return pw_tight(K) || PW_LATE_B_ALL; }
+#ifndef PW_QUAD4
+#define PW_QUAD4 0        // A/B builds: the quad loader's four inputs in flight at once
+#endif
 
 __host__ __device__ constexpr size_t pw_lds_bytes(int M, int K, int l)
 {
@@ -595,6 +601,18 @@ __device__ __forceinline__ void pw_load_quad_bfly(u64 (&L)[M], int &T, const u64
             acc[j] = ((u64)hi << 32) | lo;
         }
     };
+    if (PW_QUAD4) {   // all four inputs' bytes in flight at once
+        const int pr = pos >= 2 ? tr : t;
+        PwRaw<LP> R0, R1, R2, R3;
+        pw_piece_fetch<LP>(R0, dig + (size_t)s0 * l, cb + (size_t)s0 * cbw, top + s0, l, t);
+        pw_piece_fetch<LP>(R2, dig + (size_t)(s0 + 2) * l, cb + (size_t)(s0 + 2) * cbw, top + s0 + 2, l, t);
+        pw_piece_fetch<LP>(R1, dig + (size_t)(s0 + 1) * l, cb + (size_t)(s0 + 1) * cbw, top + s0 + 1, l, pr);
+        pw_piece_fetch<LP>(R3, dig + (size_t)(s0 + 3) * l, cb + (size_t)(s0 + 3) * cbw, top + s0 + 3, l, pr);
+        add(R0, 0, t);
+        add(R2, 2, t);
+        add(R1, 1, pr);
+        add(R3, 3, pr);
+    } else
     // two inputs' bytes in flight at a time (x0, x2 at piece t; then x1, x3)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -769,6 +787,8 @@ __device__ __forceinline__ void pw_slot_output(const u64 *X, const int *TT, int 
 // (mul_fft.c:2392-2408's last FFT_radix2 level fused into the pointwise loop :3244-3253,
 // cf. the reference's row/pointwise fusion IFFT_radix2_mfa_truncate_sqrt2_combined :2745).
 // Both workgroups of a pair read all four inputs, so the product goes to C, not in place.
+// FUSE 2: the last two levels on slot quads (pw_load_quad_bfly), the four workgroups of a quad
+// on one XCD.
 // (Fusing the inverse row DIT's first level as well needs both products in one workgroup:
 // measured at 194-256 VGPRs, occupancy 2 -> 1, so the inverse side stays a pass.)
 template <int M, int LK, int FUSE>
