@@ -152,6 +152,9 @@ int mpfft_shard_row_fused(long n1, long n2, unsigned long depth, unsigned long w
 #define MPFFT_SHARD_FWD_COLUMNS_A 5 /* MPFFT_SHARD_FWD_COLUMNS for operand 1 only (clears the combine flags) */
 #define MPFFT_SHARD_FWD_COLUMNS_B 6 /* ... for operand 2 only: with _A, lets operand 1's exchange overlap it */
 int mpfft_shard_stage(int stage, const mpfft_shard *sh, const uint64_t *d_i1, const uint64_t *d_i2, void *stream);
+/* The row stages (FWD_ROWS, POINTWISE, INV_ROWS) on local rows [lo, hi) of the shard only, so a
+ * driver can run the row phase in chunks and start exchange #2 of a finished chunk early. */
+int mpfft_shard_stage_rows(int stage, const mpfft_shard *sh, int lo, int hi, void *stream);
 
 /* Combine the canonical coefficients of the row layout (A) into product limbs
  * [m0, m0+mcount).  kbase = r0 * NC is the first local coefficient; halo holds the

@@ -109,6 +109,8 @@ def lib():
         h.mpfft_fill_random.restype = None
         h.mpfft_shard_stage.argtypes = [ctypes.c_int, ctypes.POINTER(_Shard), _vp, _vp, _vp]
         h.mpfft_shard_stage.restype = ctypes.c_int
+        h.mpfft_shard_stage_rows.argtypes = [ctypes.c_int, ctypes.POINTER(_Shard), ctypes.c_int, ctypes.c_int, _vp]
+        h.mpfft_shard_stage_rows.restype = ctypes.c_int
         h.mpfft_shard_row_fused.argtypes = [_L, _L, _UL, _UL, ctypes.c_int]
         h.mpfft_shard_row_fused.restype = ctypes.c_int
         h.mpfft_shard_combine_tmp_bytes.argtypes = [_L]
@@ -400,6 +402,13 @@ def shard_stage(which, desc, d_i1, d_i2, stream=None):
     rc = lib().mpfft_shard_stage(which, ctypes.byref(desc), _ptr(d_i1), _ptr(d_i2), _stream(stream))
     if rc:
         raise MpfftError(rc, f"mpfft_shard_stage({which})")
+
+
+def shard_stage_rows(which, desc, lo, hi, stream=None):
+    """The row stages (SHARD_FWD_ROWS / POINTWISE / INV_ROWS) on local rows [lo, hi) only."""
+    rc = lib().mpfft_shard_stage_rows(which, ctypes.byref(desc), lo, hi, _stream(stream))
+    if rc:
+        raise MpfftError(rc, f"mpfft_shard_stage_rows({which}, {lo}, {hi})")
 
 
 def shard_combine_tmp_bytes(mcount):

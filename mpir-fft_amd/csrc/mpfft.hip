@@ -775,9 +775,11 @@ struct Exec {
         return lk && pw_get(pw_inner_limbs(P.l, lk), lk) != nullptr;
     }
 
+    long pw_count = 0;   // > 0: the pointwise covers this many slots from the row views (a row chunk of one column block)
+
     int pointwise()
     {
-        const long cnt = (long)rcount * P.NC;
+        const long cnt = pw_count > 0 ? pw_count : (long)rcount * P.NC;
         if (cnt == 0) return MPFFT_OK;
         if (const int lk = pwss_lk(P.l)) {
             const int M = pw_inner_limbs(P.l, lk);
@@ -1595,6 +1597,48 @@ static int shard_exec(Exec &X, const mpfft_shard *sh)
         X.cview.cb[0] = sh->rowc_cb;
         X.cview.top[0] = sh->rowc_top;
         X.fuse_row_last = true;
+    }
+    return MPFFT_OK;
+}
+
+// The row stages on local rows [lo, hi) only (a row chunk: its exchange #2 can start while the
+// next chunk computes).  The row layout keeps its block stride (rcount ccb slots per column
+// block); the row passes take the chunk through their row offset and count, the pointwise is
+// launched once per column block on the chunk's contiguous slots.
+int mpfft_shard_stage_rows(int stage, const mpfft_shard *sh, int lo, int hi, void *stream)
+{
+    Plan P;
+    int rc = make_plan(&P, sh->n1, sh->n2, sh->depth, sh->w);
+    if (rc) return rc;
+    if (lo < 0 || hi > sh->rcount || lo > hi) return MPFFT_EINVAL;
+    if (stage != MPFFT_SHARD_FWD_ROWS && stage != MPFFT_SHARD_POINTWISE && stage != MPFFT_SHARD_INV_ROWS)
+        return MPFFT_EINVAL;
+    if (lo == hi) return MPFFT_OK;
+    (void)hipGetLastError();
+    Exec X(P, (hipStream_t)stream);
+    if ((rc = shard_exec(X, sh))) return rc;
+    const long cbw = cb_words((int)P.l);
+    auto shift = [&](View &v, long slots, int nk) {
+        for (int k = 0; k < nk; ++k)
+            if (v.dig[k]) {
+                v.dig[k] += slots * P.l;
+                v.cb[k] += slots * cbw;
+                v.top[k] += slots;
+            }
+    };
+    // X.cbs (the block stride) stays the full rcount ccb
+    shift(X.row, (long)lo * X.ccb, 2);
+    shift(X.cview, (long)lo * X.ccb, 1);
+    X.r0 += lo;
+    X.rcount = hi - lo;
+    if (stage == MPFFT_SHARD_FWD_ROWS) return X.fwd_rows(2);
+    if (stage == MPFFT_SHARD_INV_ROWS) return X.inv_rows();
+    for (long b = 0; b < P.NC / X.ccb; ++b) {   // the pointwise: one launch per column block
+        Exec Y = X;
+        shift(Y.row, b * X.cbs, 2);
+        shift(Y.cview, b * X.cbs, 1);
+        Y.pw_count = (long)(hi - lo) * X.ccb;
+        if ((rc = Y.pointwise())) return rc;
     }
     return MPFFT_OK;
 }

@@ -23,6 +23,8 @@ use all_to_all_single (RCCL over xGMI on GPUs, gloo on CPU for the tests);
 no all-reduce is used.  Each exchange moves one copy of the data: #1 both
 operands, #2 and #3 one.
 """
+import os
+
 import numpy as np
 
 
@@ -99,6 +101,10 @@ class ShardedMul:
     """One rank's part.  `backend` runs the stages on this rank's buffers,
     `comm` moves them (both duck-typed; see GpuBackend / TorchComm)."""
 
+    # world > 1: the row phase in this many row chunks (exchange #2 overlapped); MPFFT_ROW_CHUNKS
+    # overrides (diagnostics / A/B)
+    row_chunks = int(os.environ.get("MPFFT_ROW_CHUNKS", "4"))
+
     def __init__(self, plan, rank, backend, comm, sliced=True):
         self.p, self.rank, self.be, self.comm = plan, rank, backend, comm
         self.sliced = sliced          # run() gets this rank's operand slices (ShardPlan.slice_operand)
@@ -126,7 +132,7 @@ class ShardedMul:
     def shard_desc(self):
         p, d = self.p, self.rank
         return dict(n1=p.n1, n2=p.n2, depth=p.depth, w=p.w, c0=d * p.C, ccount=p.C,
-                    r0=p.rows[d], rcount=p.rcount(d), ccb=p.C, col=self.col, row=self.row,
+                    r0=p.rows[d], rcount=p.rcount(d), ccb=p.C, col=list(self.col), row=list(self.row),
                     src_chunk=p.chunk if self.sliced else 0, rowc=self.rowc)
 
     # one exchange from the library's copy plan (the same copies mpfft_mul_multi issues as
@@ -136,9 +142,11 @@ class ShardedMul:
     # point-to-point ops
     _FIELDS = ("dig", "cb", "top")
 
-    def _exchange(self, which, op=None, wait=True):
+    def _exchange(self, which, op=None, wait=True, chunk=None):
         """op: only that operand's copies; wait=False: returns the pending transfers
-        (comm.wait them later), so compute queued meanwhile overlaps the exchange."""
+        (comm.wait them later), so compute queued meanwhile overlaps the exchange.
+        chunk = (i, R): exchange #2 for row chunk i of R of every row-layout rank (rows are
+        contiguous, C slots each, on both sides of every copy)."""
         p, me = self.p, self.rank
         W = p.world
 
@@ -148,6 +156,14 @@ class ShardedMul:
         for c in p.exchange_plan(which):
             if me not in (c["src"], c["dst"]) or (op is not None and c["op"] != op):
                 continue
+            if chunk is not None:   # this chunk's rows of the row-layout rank (the sender of #2)
+                d = c["src"] if which == XCHG_ROW_TO_COL else c["dst"]
+                rc_d = p.rcount(d)
+                a_, b_ = chunk_rows(rc_d, *chunk)
+                per = c["count"] // rc_d          # C slots x field width per row
+                c = dict(c, src_off=c["src_off"] + a_ * per, dst_off=c["dst_off"] + a_ * per, count=(b_ - a_) * per)
+                if not c["count"]:
+                    continue
             f = self._FIELDS[c["field"]]
             send, recv = groups.setdefault((c["op"], c["field"]), ([None] * W, [None] * W))
             if c["src"] == me:
@@ -166,6 +182,7 @@ class ShardedMul:
         operands when sliced=False), backend arrays.  Returns (m0, limbs).
         mark(name), when given, is called after each phase (bench.py's per-phase events)."""
         p, be, sh = self.p, self.be, self.shard_desc()
+        chunked_ok = mark is None
         mark = mark or (lambda name: None)
         if getattr(be, "split_columns", False):
             # operand 1's exchange in flight while operand 2's column passes run (on RCCL: the
@@ -181,18 +198,38 @@ class ShardedMul:
             mark("fwd_columns")
             self._exchange(XCHG_COL_TO_ROW)
         mark("exchange1")
-        be.stage("fwd_rows", sh, i1, i2)
-        mark("fwd_rows")
-        be.stage("pointwise", sh, i1, i2)
-        mark("pointwise")
-        if self.fused:   # the product is in rowc: it becomes operand 0's row array
-            self.row[0], self.rowc = self.rowc, self.row[0]
-            if self.colc is not None:   # world 1: and its column array operand 0's
-                self.col[0], self.colc = self.colc, self.col[0]
-            sh = self.shard_desc()
-        be.stage("inv_rows", sh, i1, i2)
-        mark("inv_rows")
-        self._exchange(XCHG_ROW_TO_COL)
+        # (a run with per-phase marks -- bench.py's phase breakdown -- keeps the phases whole)
+        R = self.row_chunks if (p.world > 1 and hasattr(be, "stage_rows") and chunked_ok) else 1
+        if R > 1:
+            # the row phase in R row chunks, each chunk's exchange #2 in flight while the next
+            # computes (chunk i of every rank: chunk_rows; the senders' chunking is known to all)
+            sh_fwd = sh      # (its own copies of the array lists: the swap below leaves it as it is)
+            if self.fused:
+                self.row[0], self.rowc = self.rowc, self.row[0]
+            sh_inv = self.shard_desc()   # operand 0's row array = the product
+            pend = []
+            for i in range(R):
+                lo, hi = chunk_rows(p.rcount(self.rank), i, R)
+                be.stage_rows("fwd_rows", sh_fwd, lo, hi)
+                be.stage_rows("pointwise", sh_fwd, lo, hi)
+                be.stage_rows("inv_rows", sh_inv, lo, hi)
+                pend += self._exchange(XCHG_ROW_TO_COL, wait=False, chunk=(i, R))
+            mark("inv_rows")
+            self.comm.wait(pend)
+            sh = sh_inv
+        else:
+            be.stage("fwd_rows", sh, i1, i2)
+            mark("fwd_rows")
+            be.stage("pointwise", sh, i1, i2)
+            mark("pointwise")
+            if self.fused:   # the product is in rowc: it becomes operand 0's row array
+                self.row[0], self.rowc = self.rowc, self.row[0]
+                if self.colc is not None:   # world 1: and its column array operand 0's
+                    self.col[0], self.colc = self.colc, self.col[0]
+                sh = self.shard_desc()
+            be.stage("inv_rows", sh, i1, i2)
+            mark("inv_rows")
+            self._exchange(XCHG_ROW_TO_COL)
         mark("exchange2")
         be.stage("inv_columns", sh, i1, i2)
         mark("inv_columns")
@@ -213,6 +250,11 @@ class ShardedMul:
         limbs = be.combine(sh, 1, m0, mcount, kbase, halo, p.H if d else 0, cin=cin)
         mark("combine")
         return m0, limbs
+
+
+def chunk_rows(rcount, i, R):
+    """local rows of chunk i of R of a rank holding rcount rows"""
+    return rcount * i // R, rcount * (i + 1) // R
 
 
 def _same_view(a, b):
@@ -316,6 +358,11 @@ class GpuBackend:
         return self.mp.shard_desc(sh)
 
     split_columns = True   # per-operand forward column stages (exchange #1 overlaps operand 2's)
+
+    def stage_rows(self, name, sh, lo, hi):
+        """a row stage on local rows [lo, hi) (the chunked row phase)"""
+        which = {"fwd_rows": 1, "pointwise": 2, "inv_rows": 3}[name]
+        self.mp.shard_stage_rows(which, self._desc(sh), lo, hi, self.stream)
 
     def stage(self, name, sh, i1, i2):
         which = {"fwd_columns": 0, "fwd_rows": 1, "pointwise": 2, "inv_rows": 3, "inv_columns": 4,

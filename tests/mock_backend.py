@@ -93,11 +93,15 @@ class MockBackend:
                     v = sum(x * self.pw(p.w * p.NC * jr * kr) for jr, x in enumerate(xs) if x)
                     self.put(sh["col"][k], self.col_slot(sh, pos, cl), v)
 
-    def _fwd_rows(self, sh, i1, i2):
+    def stage_rows(self, name, sh, lo, hi):
+        """a row stage on local rows [lo, hi) (the chunked row phase, GpuBackend.stage_rows)"""
+        getattr(self, "_" + name)(sh, None, None, rows=range(lo, hi))
+
+    def _fwd_rows(self, sh, i1, i2, rows=None):
         p = self.p
         for k in (0, 1):
             buf = sh["row"][k]
-            for pl in range(sh["rcount"]):
+            for pl in (rows if rows is not None else range(sh["rcount"])):
                 kr = revbin(sh["r0"] + pl, self.lbR)
                 y = [self.get(buf, self.row_slot(sh, pl, c)) * self.pw(p.w * c * kr) for c in range(p.NC)]
                 for q in range(p.NC):
@@ -105,15 +109,17 @@ class MockBackend:
                     self.put(buf, self.row_slot(sh, pl, q),
                              sum(y[c] * self.pw(p.w * p.NR * c * kc) for c in range(p.NC)))
 
-    def _pointwise(self, sh, i1, i2):
+    def _pointwise(self, sh, i1, i2, rows=None):
         A, B = sh["row"]
-        for s in range(sh["rcount"] * self.p.NC):
-            self.put(A, s, self.get(A, s) * self.get(B, s))
+        for pl in (rows if rows is not None else range(sh["rcount"])):
+            for c in range(self.p.NC):
+                s = self.row_slot(sh, pl, c)
+                self.put(A, s, self.get(A, s) * self.get(B, s))
 
-    def _inv_rows(self, sh, i1, i2):
+    def _inv_rows(self, sh, i1, i2, rows=None):
         p = self.p
         buf = sh["row"][0]
-        for pl in range(sh["rcount"]):
+        for pl in (rows if rows is not None else range(sh["rcount"])):
             kr = revbin(sh["r0"] + pl, self.lbR)
             x = [self.get(buf, self.row_slot(sh, pl, q)) for q in range(p.NC)]
             for c in range(p.NC):
