@@ -105,9 +105,14 @@ class ShardedMul:
     # overrides (diagnostics / A/B)
     row_chunks = int(os.environ.get("MPFFT_ROW_CHUNKS", "4"))
 
-    def __init__(self, plan, rank, backend, comm, sliced=True):
+    def __init__(self, plan, rank, backend, comm, sliced=True, replicate=False):
         self.p, self.rank, self.be, self.comm = plan, rank, backend, comm
         self.sliced = sliced          # run() gets this rank's operand slices (ShardPlan.slice_operand)
+        # replicate: every rank computes every column block's forward columns from the whole
+        # operands and keeps its own rows of each, so exchange #1 moves nothing (see replicates)
+        if replicate and sliced:
+            raise ValueError("replicated forward columns need the whole operands (sliced=False)")
+        self.replicate = replicate
         p = plan
         self.col = [backend.alloc_coeffs(p.col_slots()) for _ in range(2)]
         if p.world == 1:
@@ -128,6 +133,19 @@ class ShardedMul:
             self.rowc = {f: self.colc[f][: p.row_slots(rank) * backend.width(f, p)] for f in self.colc}
         else:
             self.rowc = backend.alloc_coeffs(p.row_slots(rank)) if self.fused else None
+
+    @staticmethod
+    def replicates(world):
+        """the forward-column policy for `world` ranks: replicated at world 2, where exchange
+        #1 is one xGMI link carrying half of both operands' coefficient arrays each way (C4:
+        ≈ 5 GB, ≈ 65 ms at 76 GB/s) and the second column block costs one more column phase
+        of HBM-bound passes (C4: ≈ 9 ms); at world 4 the exchange spreads over three links
+        (≈ 1.9 GB per rank) and replication would cost three blocks (≈ 14 ms), so the columns
+        stay sharded.  MPFFT_REPLICATE_COLUMNS=0/1 overrides (A/B)."""
+        env = os.environ.get("MPFFT_REPLICATE_COLUMNS")
+        if env is not None:
+            return env == "1" and world > 1
+        return world == 2
 
     def shard_desc(self):
         p, d = self.p, self.rank
@@ -184,7 +202,21 @@ class ShardedMul:
         p, be, sh = self.p, self.be, self.shard_desc()
         chunked_ok = mark is None
         mark = mark or (lambda name: None)
-        if getattr(be, "split_columns", False):
+        if self.replicate:
+            # every column block's forward columns here in turn (the column arrays are scratch
+            # for the block being computed), then this rank's rows of that block copied to its
+            # row layout: exchange #1's copies with every source rank played locally
+            recv = [c for c in p.exchange_plan(XCHG_COL_TO_ROW) if c["dst"] == self.rank]
+            for d in range(p.world):
+                be.stage("fwd_columns", dict(sh, c0=d * p.C), i1, i2)
+                for c in recv:
+                    if c["src"] == d:
+                        f = self._FIELDS[c["field"]]
+                        src = (self.row if c["src_layout"] else self.col)[c["op"]][f]
+                        dst = (self.row if c["dst_layout"] else self.col)[c["op"]][f]
+                        dst[c["dst_off"]: c["dst_off"] + c["count"]].copy_(src[c["src_off"]: c["src_off"] + c["count"]])
+            mark("fwd_columns")
+        elif getattr(be, "split_columns", False):
             # operand 1's exchange in flight while operand 2's column passes run (on RCCL: the
             # transfers go on the communicator's stream, queued behind operand 1's passes only)
             be.stage("fwd_columns_a", sh, i1, i2)
@@ -423,16 +455,19 @@ def bench(args, cfg_name, cfg, rank, world, dev):
     plan = ShardPlan(mp, nl, nl, depth, w, world)
     a = mp.fill_random(nl, 0x1001)
     b = mp.fill_random(nl, 0x2002)
-    # only this rank's column slices of the operands travel to its GPU (1/world of each)
-    ha = plan.slice_operand(a, rank)
-    hb = plan.slice_operand(b, rank)
+    rep = ShardedMul.replicates(world)
+    if rep:   # replicated forward columns: the whole operands on every rank
+        ha, hb = a, b
+    else:     # only this rank's column slices of the operands travel to its GPU (1/world of each)
+        ha = plan.slice_operand(a, rank)
+        hb = plan.slice_operand(b, rank)
     del a, b
     da = torch.from_numpy(ha.view(np.int64)).to(dev)
     db = torch.from_numpy(hb.view(np.int64)).to(dev)
     be = GpuBackend(mp, plan, dev)
     rccl = world > 1 and dist.get_backend() == "nccl"
     comm = TorchComm(host_staging=(world > 1 and not rccl)) if world > 1 else _SoloComm()
-    job = ShardedMul(plan, rank, be, comm)
+    job = ShardedMul(plan, rank, be, comm, sliced=not rep, replicate=rep)
 
     def sync_all():
         torch.cuda.synchronize(dev)
@@ -540,8 +575,11 @@ def bench(args, cfg_name, cfg, rank, world, dev):
             "data": "synthetic (xoshiro256** limbs, seeds 0x1001/0x2002)",
             "config": {"workload": f"{cfg_name}: sharded new_mpn_mul depth={depth} w={w} n1=n2={nl} limbs "
                                    f"(l={P['l']}, NC x NR = {P['NC']} x {P['NR']}, trunc={P['trunc']})",
-                       "parallelism": f"MFA columns x{world}, operand column slices, 3 batched point-to-point "
-                                      f"exchanges + halo all-gather ({comm_label})",
+                       "parallelism": (f"MFA columns x{world}, " + (
+                                "forward columns replicated (whole operands on every rank), exchange #1 local; "
+                                "2 batched point-to-point exchanges" if rep else
+                                "operand column slices, 3 batched point-to-point exchanges") +
+                                f" + halo all-gather ({comm_label})"),
                        "row_fused": job.fused},
             "roofline": roof,
             "phases_ms": phase_ms,
@@ -552,7 +590,7 @@ def bench(args, cfg_name, cfg, rank, world, dev):
                              "note": "timed on the N = 1 line only (rank 0, bounded sample: the bench contract); "
                                      "see BENCH_rNN.json cpu_baseline"},
             "e2e_host": {"ms": e2e_ms, "limbs_per_s": 2 * nl / (e2e_ms * 1e-3),
-                         "note": "per rank: its operand column slices H2D, the multiply, its product limbs D2H "
+                         "note": "per rank: its operands (column slices, or whole when replicated) H2D, the multiply, its product limbs D2H "
                                  "(host slicing excluded); max over ranks"},
             "exact": exact}
 

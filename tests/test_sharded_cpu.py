@@ -25,7 +25,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, depth, w, n1, n2, seed, q):
+def _worker(rank, world, port, depth, w, n1, n2, seed, q, replicate=False):
     import sys
     sys.path.insert(0, os.path.dirname(HERE))
     sys.path.insert(0, HERE)
@@ -41,8 +41,11 @@ def _worker(rank, world, port, depth, w, n1, n2, seed, q):
         rng = random.Random(seed)
         a = mp.fill_random(n1, rng.getrandbits(64))
         b = mp.fill_random(n2, rng.getrandbits(64))
-        job = ShardedMul(plan, rank, MockBackend(plan), TorchComm())
-        sa, sb = plan.slice_operand(a, rank), plan.slice_operand(b, rank)   # this rank's column slices
+        job = ShardedMul(plan, rank, MockBackend(plan), TorchComm(), sliced=not replicate, replicate=replicate)
+        if replicate:   # replicated forward columns: the whole operands on every rank
+            sa, sb = a, b
+        else:
+            sa, sb = plan.slice_operand(a, rank), plan.slice_operand(b, rank)   # this rank's column slices
         m0, limbs = job.run(torch.from_numpy(sa.view(np.int64)), torch.from_numpy(sb.view(np.int64)))
         # gather the distributed product on every rank
         sizes = [plan.M[d + 1] - plan.M[d] for d in range(world)]
@@ -62,11 +65,12 @@ def _worker(rank, world, port, depth, w, n1, n2, seed, q):
         dist.destroy_process_group()
 
 
-def _run(world, depth, w, n1, n2, seed=1):
+def _run(world, depth, w, n1, n2, seed=1, replicate=False):
     ctx = tmp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, depth, w, n1, n2, seed, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, depth, w, n1, n2, seed, q, replicate))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -86,6 +90,27 @@ def _run(world, depth, w, n1, n2, seed=1):
 ])
 def test_sharded_gloo_exact(world, depth, w, n1, n2):
     _run(world, depth, w, n1, n2)
+
+
+@pytest.mark.parametrize("world,depth,w,n1,n2", [
+    (2, 6, 2, 7, 6),       # world 2 (the replicated policy's world), full truncation variety
+    (2, 8, 2, 50, 3),      # unbalanced operands
+    (4, 8, 1, 100, 90),    # forced at 4 ranks (MPFFT_REPLICATE_COLUMNS=1)
+])
+def test_sharded_gloo_replicated_columns(world, depth, w, n1, n2):
+    """every rank computes every column block from the whole operands and keeps its rows:
+    exchange #1 played locally (ShardedMul.replicate)"""
+    _run(world, depth, w, n1, n2, seed=3, replicate=True)
+
+
+def test_replicate_policy(mp, monkeypatch):
+    from mpir_fft_amd.sharded import ShardedMul
+    monkeypatch.delenv("MPFFT_REPLICATE_COLUMNS", raising=False)
+    assert [ShardedMul.replicates(W) for W in (1, 2, 4, 8)] == [False, True, False, False]
+    monkeypatch.setenv("MPFFT_REPLICATE_COLUMNS", "0")
+    assert not ShardedMul.replicates(2)
+    monkeypatch.setenv("MPFFT_REPLICATE_COLUMNS", "1")
+    assert ShardedMul.replicates(8) and not ShardedMul.replicates(1)
 
 
 def test_shard_plan_partition(mp):

@@ -85,7 +85,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, depth, w, n1, n2, q):
+def _worker(rank, world, port, depth, w, n1, n2, q, replicate=False):
     import sys
     sys.path.insert(0, os.path.dirname(HERE))
     sys.path.insert(0, HERE)
@@ -103,8 +103,12 @@ def _worker(rank, world, port, depth, w, n1, n2, q):
         plan = ShardPlan(mp, n1, n2, depth, w, world)
         a = mp.fill_random(n1, 0x1001)
         b = mp.fill_random(n2, 0x2002)
-        job = ShardedMul(plan, rank, GpuBackend(mp, plan, dev), TorchComm(host_staging=True))
-        sa, sb = plan.slice_operand(a, rank), plan.slice_operand(b, rank)   # this rank's column slices
+        job = ShardedMul(plan, rank, GpuBackend(mp, plan, dev), TorchComm(host_staging=True),
+                         sliced=not replicate, replicate=replicate)
+        if replicate:   # replicated forward columns: the whole operands on every rank
+            sa, sb = a, b
+        else:
+            sa, sb = plan.slice_operand(a, rank), plan.slice_operand(b, rank)   # this rank's column slices
         m0, limbs = job.run(torch.from_numpy(sa.view(np.int64)).to(dev), torch.from_numpy(sb.view(np.int64)).to(dev))
         limbs = limbs.cpu()
         sizes = [plan.M[d + 1] - plan.M[d] for d in range(world)]
@@ -132,11 +136,24 @@ def _worker(rank, world, port, depth, w, n1, n2, q):
                                                  (4, 13, 32, 1000000, 1000000), (8, 13, 32, 1000000, 1000000),
                                                  (8, 15, 4, 2000000, 1900000)])
 def test_sharded_ranks_one_gpu(world, depth, w, n1, n2):
+    _ranks_one_gpu(world, depth, w, n1, n2)
+
+
+# replicated forward columns (bench.py's policy at world 2): every column block computed from
+# the whole operands on each rank, exchange #1 local; l = 2048 and l = 4096, and 4 ranks forced
+@pytest.mark.parametrize("world,depth,w,n1,n2", [(2, 15, 4, 2000000, 2000000), (2, 13, 32, 1000000, 1000000),
+                                                 (2, 9, 2, 2000, 1500), (4, 13, 32, 1000000, 1000000)])
+def test_sharded_ranks_one_gpu_replicated(world, depth, w, n1, n2):
+    _ranks_one_gpu(world, depth, w, n1, n2, replicate=True)
+
+
+def _ranks_one_gpu(world, depth, w, n1, n2, replicate=False):
     import torch.multiprocessing as tmp
     ctx = tmp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, depth, w, n1, n2, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, depth, w, n1, n2, q, replicate))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
