@@ -9,6 +9,8 @@
 //   H2D       rank g's operand column slices (packed on the host, one thread per rank)
 //   stage     split + forward column passes                   (mpfft_shard_stage)
 //   xchg #1   column layout -> row layout, both operands      (peer copies over xGMI)
+//             -- at two ranks both compute every column block instead (all blocks' slices
+//             H2D) and keep their rows of each: exchange #1 becomes local copies
 //   stage     forward rows, pointwise, inverse rows
 //   xchg #2   row layout -> column layout, the product
 //   stage     truncated inverse columns + scale
@@ -43,6 +45,8 @@ struct Part {
     long n1, n2, total, n, l, NC, NR, T, Tr, bits1, N, len;
     long C, chunk, H, cbw;
     bool fused;
+    bool rep;      // replicated forward columns: every rank computes every column block (world 2)
+    long nsl() const { return rep ? world : 1; }   // operand column slices a rank holds
     std::vector<long> rows, M;
     long rcount(int d) const { return rows[d + 1] - rows[d]; }
 };
@@ -87,6 +91,7 @@ int partition(Part &p, long n1, long n2, unsigned long depth, unsigned long w, i
     if (p.Tr < world) return MPFFT_EINVAL;
     p.chunk = (p.C * p.bits1 + 63) / 64 + 2;
     p.fused = mpfft_shard_row_fused(n1, n2, depth, w, (int)p.C) != 0;
+    p.rep = false;
     return MPFFT_OK;
 }
 
@@ -183,7 +188,8 @@ int setup_rank(const Part &p, int d, Rank &R)
     const int nrow = w1 ? 0 : (p.fused ? 3 : 2);      // world 1: row arrays are views
     auto arr_bytes = [&](long slots) { return al(slots * p.l * 8) + al(slots * p.cbw * 8) + al(slots * 4); };
     const size_t tmpb = mpfft_shard_combine_tmp_bytes(mcount > 0 ? mcount : 1);
-    const size_t need = ncol * arr_bytes(cs) + nrow * arr_bytes(rs) + 2 * al(p.Tr * p.chunk * 8) +
+    const long sl = p.nsl() * p.Tr * p.chunk;        // operand slices held (all blocks' when replicated)
+    const size_t need = ncol * arr_bytes(cs) + nrow * arr_bytes(rs) + 2 * al(sl * 8) +
                         al(p.H * p.l * 8) + al((mcount > 0 ? mcount : 1) * 8) + al(tmpb) + 256;
     if (R.mem_bytes < need) {
         if (R.mem) MCHK(hipFree(R.mem));
@@ -213,14 +219,14 @@ int setup_rank(const Part &p, int d, Rank &R)
         R.row[1] = carve(rs);
         R.rowc = p.fused ? carve(rs) : Arr();
     }
-    R.src[0] = (u64 *)q; q += al(p.Tr * p.chunk * 8);
-    R.src[1] = (u64 *)q; q += al(p.Tr * p.chunk * 8);
+    R.src[0] = (u64 *)q; q += al(sl * 8);
+    R.src[1] = (u64 *)q; q += al(sl * 8);
     R.halo = (u64 *)q; q += al(p.H * p.l * 8);
     R.r = (u64 *)q; q += al((mcount > 0 ? mcount : 1) * 8);
     R.tmp = q; q += al(tmpb);
     R.tmp_bytes = tmpb;
     R.sum = (int *)q;
-    const size_t hb = (size_t)2 * p.Tr * p.chunk * 8;
+    const size_t hb = (size_t)2 * sl * 8;
     if (R.host_bytes < hb) {
         if (R.host) MCHK(hipHostFree(R.host));
         R.host = nullptr;
@@ -303,6 +309,36 @@ int queue_copy(const std::vector<Rank> &rk, const mpfft_copy &c, hipStream_t st)
 // stream pulls operand 1's blocks once all senders finished operand 1's passes (event eva)
 // -- while the compute streams run operand 2's passes -- then operand 2's (event ev); the
 // compute stream waits for both before the row passes
+int run_exchange_fwd(const Part &p, std::vector<Rank> &rk);
+
+// replicated forward columns (world 2): rank d runs every column block e's split + column
+// passes from block e's operand slices into its own column arrays (scratch), then plays
+// exchange #1's copies from e to d locally -- its rows of block e into its row layout
+int fwd_replicated(const Part &p, std::vector<Rank> &rk, unsigned long depth, unsigned long w)
+{
+    std::vector<mpfft_copy> plan;
+    exchange_plan(p, MPFFT_XCHG_COL_TO_ROW, plan);
+    const long sl = p.Tr * p.chunk;
+    for (int d = 0; d < p.world; ++d) {
+        Rank &R = rk[d];
+        MCHK(hipSetDevice(R.dev));
+        for (int e = 0; e < p.world; ++e) {
+            mpfft_shard sh = desc(p, d, R, depth, w);
+            sh.c0 = (int)(e * p.C);
+            int rc = mpfft_shard_stage(MPFFT_SHARD_FWD_COLUMNS, &sh, R.src[0] + e * sl, R.src[1] + e * sl, R.s);
+            if (rc) return rc;
+            for (const mpfft_copy &c : plan)
+                if (c.dst == d && c.src == e) {
+                    mpfft_copy m = c;
+                    m.src = d;          // block e's column layout is rank d's own column arrays now
+                    if ((rc = queue_copy(rk, m, R.s))) return rc;
+                }
+        }
+        MCHK(hipEventRecord(R.ev, R.s));
+    }
+    return MPFFT_OK;
+}
+
 int run_exchange_fwd(const Part &p, std::vector<Rank> &rk)
 {
     std::vector<mpfft_copy> plan;
@@ -388,6 +424,13 @@ int mul_multi_locked(Ctx &X, uint64_t *r1, const uint64_t *i1, long n1, const ui
     const int G = (int)devs.size();
     int rc = partition(p, n1, n2, depth, w, G);
     if (rc) return rc;
+    // replicated forward columns at two ranks (sharded.py ShardedMul.replicates: exchange #1
+    // there is one xGMI link carrying half of both coefficient arrays; the second column block
+    // is one more column phase of HBM-bound passes); MPFFT_REPLICATE_COLUMNS=0/1 overrides
+    {
+        const char *e = getenv("MPFFT_REPLICATE_COLUMNS");
+        p.rep = e ? (e[0] == '1' && G > 1) : G == 2;
+    }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return MPFFT_ENODEV;
     for (int d : devs)
@@ -410,12 +453,16 @@ int mul_multi_locked(Ctx &X, uint64_t *r1, const uint64_t *i1, long n1, const ui
         for (int d = 0; d < G; ++d)
             th.emplace_back([&, d] {
                 Rank &R = rk[d];
-                u64 *h0 = R.host, *h1 = R.host + p.Tr * p.chunk;
-                pack_slice(p, d, i1, n1, h0);
-                pack_slice(p, d, i2, n2, h1);
+                const long sl = p.Tr * p.chunk, ns = p.nsl();
+                u64 *h0 = R.host, *h1 = R.host + ns * sl;
+                for (long e = 0; e < ns; ++e) {   // replicated: every block's slices, block e at e sl
+                    const int blk = p.rep ? (int)e : d;
+                    pack_slice(p, blk, i1, n1, h0 + e * sl);
+                    pack_slice(p, blk, i2, n2, h1 + e * sl);
+                }
                 if (hipSetDevice(R.dev) != hipSuccess ||
-                    hipMemcpyAsync(R.src[0], h0, (size_t)p.Tr * p.chunk * 8, hipMemcpyHostToDevice, R.s) != hipSuccess ||
-                    hipMemcpyAsync(R.src[1], h1, (size_t)p.Tr * p.chunk * 8, hipMemcpyHostToDevice, R.s) != hipSuccess)
+                    hipMemcpyAsync(R.src[0], h0, (size_t)ns * sl * 8, hipMemcpyHostToDevice, R.s) != hipSuccess ||
+                    hipMemcpyAsync(R.src[1], h1, (size_t)ns * sl * 8, hipMemcpyHostToDevice, R.s) != hipSuccess)
                     trc[d] = MPFFT_EHIP;
             });
         for (auto &t : th) t.join();
@@ -423,9 +470,13 @@ int mul_multi_locked(Ctx &X, uint64_t *r1, const uint64_t *i1, long n1, const ui
             if (trc[d]) return trc[d];
     }
 
-    if ((rc = stage_all(p, rk, MPFFT_SHARD_FWD_COLUMNS_A, depth, w, true))) return rc;
-    if ((rc = stage_all(p, rk, MPFFT_SHARD_FWD_COLUMNS_B, depth, w))) return rc;
-    if ((rc = run_exchange_fwd(p, rk))) return rc;
+    if (p.rep) {
+        if ((rc = fwd_replicated(p, rk, depth, w))) return rc;
+    } else {
+        if ((rc = stage_all(p, rk, MPFFT_SHARD_FWD_COLUMNS_A, depth, w, true))) return rc;
+        if ((rc = stage_all(p, rk, MPFFT_SHARD_FWD_COLUMNS_B, depth, w))) return rc;
+        if ((rc = run_exchange_fwd(p, rk))) return rc;
+    }
     if ((rc = stage_all(p, rk, MPFFT_SHARD_FWD_ROWS, depth, w))) return rc;
     if ((rc = stage_all(p, rk, MPFFT_SHARD_POINTWISE, depth, w))) return rc;
     if ((rc = stage_all(p, rk, MPFFT_SHARD_INV_ROWS, depth, w))) return rc;

@@ -32,6 +32,31 @@ def test_mul_multi_one_device(mp, oracle, world, depth, w, n1, n2):
         assert (mp.mul_multi(a, b, depth, w, [0] * world) == want).all()
 
 
+@pytest.mark.parametrize("world,rep", [(2, "0"), (4, "1"), (8, "1")])
+@pytest.mark.parametrize("depth,w,n1,n2", [(13, 32, 1000000, 999000), (15, 4, 2000000, 1900000), (10, 1, 2000, 1800)])
+def test_mul_multi_column_policy_forced(mp, oracle, monkeypatch, world, rep, depth, w, n1, n2):
+    """the forward-column policy forced against its default (MPFFT_REPLICATE_COLUMNS): world 2
+    with exchange #1 over the peers, worlds 4 and 8 with every column block on every rank"""
+    monkeypatch.setenv("MPFFT_REPLICATE_COLUMNS", rep)
+    a = mp.fill_random(n1, 0x31 + depth + world)
+    b = mp.fill_random(n2, 0x42 + w)
+    assert (mp.mul_multi(a, b, depth, w, [0] * world) == oracle.gmp_mul(a, b)).all()
+
+
+def test_mul_multi_c4_world2_digest(mp):
+    """C4 over two ranks on device 0 with the default (replicated) forward columns, against the
+    GMP digest"""
+    with open(os.path.join(HERE, "golden", "products.json")) as f:
+        case = {c["name"]: c for c in json.load(f)}["C4"]
+    n1, n2, depth, w = case["n1"], case["n2"], case["depth"], case["w"]
+    a = mp.fill_random(n1, int(case["seed1"], 16))
+    b = mp.fill_random(n2, int(case["seed2"], 16))
+    r = mp.mul_multi(a, b, depth, w, [0] * 2)
+    del a, b
+    assert hashlib.sha256(r.tobytes()).hexdigest() == case["sha256"]
+    mp.multi_release()
+
+
 def test_mul_multi_c4_world8_digest(mp):
     """C4 split 8 ways exactly as on an 8-GPU node (the plan's columns and live rows dealt evenly
     over 8 ranks, seven-peer exchanges, halo, carry scan) with all ranks on device 0,
