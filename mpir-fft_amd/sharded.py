@@ -137,11 +137,12 @@ class ShardedMul:
     @staticmethod
     def replicates(world):
         """the forward-column policy for `world` ranks: replicated at world 2, where exchange
-        #1 is one xGMI link carrying half of both operands' coefficient arrays each way (C4:
-        ≈ 5 GB, ≈ 65 ms at 76 GB/s) and the second column block costs one more column phase
-        of HBM-bound passes (C4: ≈ 9 ms); at world 4 the exchange spreads over three links
-        (≈ 1.9 GB per rank) and replication would cost three blocks (≈ 14 ms), so the columns
-        stay sharded.  MPFFT_REPLICATE_COLUMNS=0/1 overrides (A/B)."""
+        #1 is one xGMI link carrying, each way, the other rank's half of both operands' column
+        blocks (C4: 2 x 1.25 GB, ≈ 33 ms at 76 GB/s) and the second column block costs one
+        more column phase of HBM-bound passes (C4: ≈ 9 ms); at world 4 the exchange spreads
+        over three links (≈ 0.63 GB per link and direction, ≈ 8 ms) and replication would cost
+        three more blocks (≈ 14 ms), so the columns stay sharded.
+        MPFFT_REPLICATE_COLUMNS=0/1 overrides (A/B)."""
         env = os.environ.get("MPFFT_REPLICATE_COLUMNS")
         if env is not None:
             return env == "1" and world > 1
