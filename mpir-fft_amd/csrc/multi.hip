@@ -425,7 +425,7 @@ int mul_multi_locked(Ctx &X, uint64_t *r1, const uint64_t *i1, long n1, const ui
     int rc = partition(p, n1, n2, depth, w, G);
     if (rc) return rc;
     // replicated forward columns at two ranks (sharded.py ShardedMul.replicates: exchange #1
-    // there is one xGMI link carrying half of both coefficient arrays; the second column block
+    // there is one xGMI link carrying the other rank's rows of both column blocks; the second column block
     // is one more column phase of HBM-bound passes); MPFFT_REPLICATE_COLUMNS=0/1 overrides
     {
         const char *e = getenv("MPFFT_REPLICATE_COLUMNS");
