@@ -209,6 +209,68 @@ def single_gpu_line(mp, dev, cfg, steps, warmup, check=True):
             "ms_per_step": el / steps * 1e3, "value": 2 * nl * steps / el, "unit": "limbs/s", "exact": exact}
 
 
+def multi_entry_line(mp, cfg, devices, steps, warmup, check=True, host_reps=1):
+    """The one-process C entry over `devices` (rank g on devices[g]; a device may repeat -- the
+    one-GPU rehearsal), as a sub-record: mpfft_mul_multi_device on packed operand slices already
+    resident on the devices (device time: K calls ordered on per-rank streams, all devices
+    synchronised around them), the stripes assembled and digest-checked, and the full
+    host-pointer mpfft_mul_multi (host packing, H2D, the multiply, D2H of the stripes)."""
+    import torch
+    depth, w, nl = CONFIGS[cfg]
+    G = len(devices)
+    part = mp.shard_partition(nl, nl, depth, w, G)
+    a = mp.fill_random(nl, SEED1)
+    b = mp.fill_random(nl, SEED2)
+    t0 = time.perf_counter()
+    packs = [(mp.shard_pack(a, nl, nl, depth, w, G, g), mp.shard_pack(b, nl, nl, depth, w, G, g)) for g in range(G)]
+    pack_ms = (time.perf_counter() - t0) * 1e3
+    devs = [torch.device("cuda", d) for d in devices]
+    src1 = [torch.from_numpy(packs[g][0].view(np.int64)).to(devs[g]) for g in range(G)]
+    src2 = [torch.from_numpy(packs[g][1].view(np.int64)).to(devs[g]) for g in range(G)]
+    del packs
+    outs = [torch.empty(part["Tr"] * part["SL"], dtype=torch.int64, device=devs[g]) for g in range(G)]
+    streams = [torch.cuda.Stream(device=devs[g]) for g in range(G)]
+
+    def sync():
+        for d in sorted(set(devices)):
+            torch.cuda.synchronize(d)
+    for _ in range(warmup):
+        mp.mul_multi_device(nl, nl, depth, w, devices, src1, src2, outs, streams=streams)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        mp.mul_multi_device(nl, nl, depth, w, devices, src1, src2, outs, streams=streams)
+    sync()
+    el = time.perf_counter() - t0
+    exact = None
+    if check:
+        prod = mp.assemble_stripes(part, G, [o.cpu().numpy().view(np.uint64) for o in outs])
+        want = golden_digest(cfg)
+        exact = hashlib.sha256(prod.tobytes()).hexdigest() == want if want else None
+        del prod
+    del src1, src2, outs
+    host_ms = None
+    if host_reps > 0:
+        mp.mul_multi(a, b, depth, w, devices)               # warm the host-pointer buffers
+        t1 = time.perf_counter()
+        for _ in range(host_reps):
+            r = mp.mul_multi(a, b, depth, w, devices)
+        host_ms = (time.perf_counter() - t1) / host_reps * 1e3
+        if check and exact is not None:
+            exact = exact and hashlib.sha256(r.tobytes()).hexdigest() == golden_digest(cfg)
+        del r
+    mp.multi_release()
+    torch.cuda.empty_cache()
+    shared = len(set(devices)) < G
+    return {"config": cfg, "path": "mpfft_mul_multi_device (one process, per-rank streams, peer copies)",
+            "devices": list(devices), "n_ranks": G, "steps": steps, "ms_per_step": el / steps * 1e3,
+            "value": 2 * nl * steps / el, "unit": "limbs/s", "exact": exact,
+            "host_pointer_ms": host_ms, "host_pack_ms_python": pack_ms,
+            "note": ("ranks sharing a device: a rehearsal of the multi-GPU schedule, not a scaling point"
+                     if shared else "device-resident operand slices; host_pointer_ms is the full mpfft_mul_multi "
+                                    "call (its own threaded packing, H2D, multiply, D2H of the stripes)")}
+
+
 def golden_digest(cfg):
     p = os.path.join(ROOT, "tests", "golden", "products.json")
     try:
@@ -237,8 +299,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default=None, choices=sorted(set(CONFIGS) | set(CONFIGS6)),
                     help="default: C3 at N = 1, C4 at N > 1 (M4: --mul6 only)")
-    ap.add_argument("--mode", default=None, choices=["single", "replicas", "sharded"],
-                    help="N > 1: sharded (default) or independent replicas")
+    ap.add_argument("--mode", default=None, choices=["single", "replicas", "sharded", "multi"],
+                    help="N > 1: sharded (default) or independent replicas; multi: the one-process C entry "
+                         "mpfft_mul_multi_device alone over --multi-ranks devices")
+    ap.add_argument("--multi-ranks", type=int, default=0, help="--mode multi: ranks (devices 0 .. K-1)")
+    ap.add_argument("--multi-share", action="store_true", help="--mode multi: every rank on device 0 (rehearsal)")
+    ap.add_argument("--no-c-entry", action="store_true",
+                    help="N > 1: skip rank 0's timing of the one-process C entry over the same devices")
     ap.add_argument("--cpu-reps", type=int, default=5, help="timed oracle calls (median; after one warm-up)")
     ap.add_argument("--cpu-warmup", type=int, default=1, help="untimed oracle calls before the timed ones")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -310,11 +377,31 @@ def main():
         if world > 1:
             dist.barrier()
         res = sh.bench(args, cfg, CONFIGS[cfg], rank, world, dev)
+        if world > 1:
+            dist.barrier()
         if rank == 0:
             res["n1_twin"] = twin
+            if not args.no_c_entry:
+                # the same product through the one-process C entry over devices 0 .. N-1 (the
+                # other ranks wait at the barrier below): a transport failure in one driver still
+                # leaves a curve from the other
+                try:
+                    devs = [0] * world if share else list(range(world))
+                    res["c_entry"] = multi_entry_line(mp, cfg, devs, max(1, min(args.steps, 3)), 1,
+                                                      check=not args.no_check)
+                except Exception as e:   # reported, never fatal to the rank-level line
+                    res["c_entry"] = {"error": repr(e)}
             print(json.dumps(res))
         if world > 1:
+            dist.barrier()
             dist.destroy_process_group()
+        return
+
+    if mode == "multi":   # the one-process C entry alone (one-GPU box: --multi-ranks K on device 0)
+        K = args.multi_ranks or 1
+        devs = [0] * K if args.multi_share else list(range(K))
+        print(json.dumps(multi_entry_line(mp, cfg, devs, args.steps, args.warmup, check=not args.no_check,
+                                          host_reps=args.e2e_reps)))
         return
 
     depth, w, nl = CONFIGS[cfg]

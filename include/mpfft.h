@@ -156,16 +156,21 @@ int mpfft_shard_stage(int stage, const mpfft_shard *sh, const uint64_t *d_i1, co
  * driver can run the row phase in chunks and start exchange #2 of a finished chunk early. */
 int mpfft_shard_stage_rows(int stage, const mpfft_shard *sh, int lo, int hi, void *stream);
 
-/* Combine the canonical coefficients of the row layout (A) into product limbs
- * [m0, m0+mcount).  kbase = r0 * NC is the first local coefficient; halo holds the
- * H coefficients before it (contiguous, l limbs each; NULL when kbase == 0).
- * phase 0: window sums + block flags; d_sum[0..1] = (carry out with carry-in 0,
- *          every limb propagates) of this rank's range.
- * phase 1: resolve with carry-in `cin` (from the ranks below) and write d_r[0..mcount). */
-size_t mpfft_shard_combine_tmp_bytes(long mcount);
-int mpfft_shard_combine(const mpfft_shard *sh, int phase, uint64_t *d_r, long m0, long mcount, long kbase,
-                        const uint64_t *halo, int H, void *d_tmp, size_t tmp_bytes, int cin, int *d_sum,
-                        void *stream);
+/* Combine the canonical coefficients of a rank's column layout (after MPFFT_SHARD_INV_COLUMNS)
+ * into its product stripes.  The product is cut into S = world * Tr stripes
+ * (mpfft_shard_partition): stripe s owns coefficients [s C, (s+1) C) and product limbs
+ * [ms[s], ms[s+1]) (mpfft_shard_stripes).  Rank g (= c0 / ccount) holds stripes s = j world + g,
+ * j < Tr -- its column-layout rows -- and writes stripe j's limbs to d_r + j SL.
+ * d_halo: the H coefficients before each of its stripes (l limbs each; stripe j's at
+ * d_halo + j H l), moved there by the copies of mpfft_shard_halo_plan.
+ * phase 0: every stripe with carry-in 0; d_sums[2 j], [2 j + 1] = (carry out, every limb
+ *          all-ones) of stripe j.
+ * phase 1: d_sums_all = the world ranks' d_sums in rank order (world * Tr * 2 ints, e.g. an
+ *          all-gather): adds the carry from the stripes below to each of the rank's stripes.
+ * Both phases are queued on `stream`; nothing synchronises with the host. */
+size_t mpfft_shard_combine_tmp_bytes(long n1, long n2, unsigned long depth, unsigned long w, int world);
+int mpfft_shard_combine(const mpfft_shard *sh, int phase, uint64_t *d_r, const uint64_t *d_halo, int *d_sums,
+                        const int *d_sums_all, void *d_tmp, size_t tmp_bytes, void *stream);
 
 /* ---- multi-GPU from one C process (north_star: "host code stays C") ----------
  * The same column-sharded multiply as mpir-fft_amd/sharded.py (one process per GPU over
@@ -173,14 +178,20 @@ int mpfft_shard_combine(const mpfft_shard *sh, int phase, uint64_t *d_r, long m0
  * stream, the three exchanges as peer copies over xGMI (hipMemcpyPeerAsync; peer access
  * enabled between distinct devices), ordered by events.
  *
- * Partition of one multiply over `world` ranks (a power of two dividing NC):
+ * Partition of one multiply over `world` ranks (a power of two dividing the plan's NC,
+ * out[2] of mpfft_plan_info -- at l = 2048 in truncation case b that is 2^(floor(depth/2)+1),
+ * not the reference's 2^floor(depth/2)):
  *   rows[world + 1]  row positions: rank d owns live rows [rows[d], rows[d+1])
- *   M[world + 1]     product limbs: rank d writes limbs [M[d], M[d+1])
- *   info[5]          C (columns per rank), chunk (operand slice limbs per row position),
- *                    H (halo coefficients), Tr (= trunc / NC), fused (1: the pointwise takes
- *                    the row DIF's last level, mpfft_shard_row_fused at ccb = C) */
+ *   info[7]          C (columns per rank), chunk (operand slice limbs per row position),
+ *                    H (halo coefficients per stripe), Tr (= trunc / NC), fused (1: the
+ *                    pointwise takes the row DIF's last level(s), mpfft_shard_row_fused at
+ *                    ccb = C), SL (product limbs per stripe at most: the d_r stride),
+ *                    S (stripes = world Tr) */
 int mpfft_shard_partition(long n1, long n2, unsigned long depth, unsigned long w, int world,
-                          long *rows, long *M, long *info);
+                          long *rows, long *info);
+/* ms[0 .. S] = the first product limb of each stripe (ms[S] = n1 + n2); returns S + 1, or
+ * -MPFFT_* (cap: ms's capacity; ms == NULL: counted only). */
+long mpfft_shard_stripes(long n1, long n2, unsigned long depth, unsigned long w, int world, long *ms, long cap);
 
 /* One exchange as element copies between the ranks' arrays (column layout: NR*C slots per
  * operand; row layout: (rows[d+1]-rows[d])*NC slots), fields dig (l u64 per slot), cb
@@ -194,19 +205,43 @@ typedef struct mpfft_copy {
 } mpfft_copy;
 #define MPFFT_XCHG_COL_TO_ROW 1   /* #1 after the forward columns: both operands, every field */
 #define MPFFT_XCHG_ROW_TO_COL 2   /* #2 after the inverse rows: operand 0, every field */
-#define MPFFT_XCHG_COEFFS 3       /* #3 after the inverse columns: operand 0's canonical limbs */
+#define MPFFT_LAYOUT_HALO 2       /* mpfft_copy.dst_layout of a halo copy: the receiver's d_halo */
 /* Number of copies written to out (out == NULL: counted only; cap: out's capacity),
  * or -MPFFT_* on error. */
 long mpfft_shard_exchange_plan(long n1, long n2, unsigned long depth, unsigned long w, int world, int which,
                                mpfft_copy *out, long cap);
+/* The halo copies before the combine: for every stripe, the H coefficients before it, from
+ * the column layout (canonical limbs, field 0) of the ranks holding them to the d_halo of
+ * mpfft_shard_combine (dst_layout MPFFT_LAYOUT_HALO); offsets and counts in limbs.  At most a
+ * few coefficients per stripe: this replaces moving the whole product to row owners. */
+long mpfft_shard_halo_plan(long n1, long n2, unsigned long depth, unsigned long w, int world,
+                           mpfft_copy *out, long cap);
 
 /* r1 = i1 * i2 (host pointers) sharded over ngpus devices: devices[g] is rank g's HIP device
  * (NULL: 0 .. ngpus-1; a device may repeat -- ranks sharing one GPU, as the tests do).
- * ngpus must be a power of two dividing NC = 2^floor(depth/2).  Device buffers are cached
- * per device list (grow-only; mpfft_multi_release frees them).  Not reentrant with itself:
- * concurrent calls serialise on one lock. */
+ * ngpus must be a power of two dividing the plan's NC (mpfft_shard_partition).  Device
+ * buffers are cached per device list (grow-only; mpfft_multi_release frees them).  Not
+ * reentrant with itself: concurrent calls serialise on one lock. */
 int mpfft_mul_multi(uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i2, long n2,
                     unsigned long depth, unsigned long w, int ngpus, const int *devices);
+
+/* The operand slices rank `rank` of `world` reads (the device-resident entry's inputs):
+ * mpfft_shard_src_limbs limbs per operand -- for each live row position q, `chunk` limbs from
+ * limb floor((q NC + c0) bits1 / 64) on, of the rank's own column block, or of every block
+ * in turn when the forward columns are replicated (two ranks; MPFFT_REPLICATE_COLUMNS). */
+long mpfft_shard_src_limbs(long n1, long n2, unsigned long depth, unsigned long w, int world);
+int mpfft_shard_pack(long n1, long n2, unsigned long depth, unsigned long w, int world, int rank,
+                     const uint64_t *a, long na, uint64_t *out);
+
+/* Device-resident multi-GPU multiply: d_src1[g], d_src2[g] are rank g's packed operand slices
+ * (mpfft_shard_pack) in devices[g]'s memory; rank g's product stripes land in d_r[g]
+ * (stripe j -- product limbs [ms[j world + g], ms[j world + g + 1]) -- at d_r[g] + j SL, Tr SL
+ * limbs).  streams[g] (hipStream_t on devices[g]): the work starts after what is queued there
+ * and is queued back onto it (nothing waits on the host); streams == NULL: the call returns
+ * when the product is complete. */
+int mpfft_mul_multi_device(long n1, long n2, unsigned long depth, unsigned long w, int ngpus, const int *devices,
+                           const uint64_t *const *d_src1, const uint64_t *const *d_src2, uint64_t *const *d_r,
+                           void *const *streams);
 int mpfft_multi_release(void);
 
 /* new_mpn_mul / mpfft_mul_ex policy: with ngpus > 1 devices set, products whose coefficients

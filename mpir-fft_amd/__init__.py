@@ -52,7 +52,8 @@ class _Copy(ctypes.Structure):
                 ("src_off", ctypes.c_long), ("dst_off", ctypes.c_long), ("count", ctypes.c_long)]
 
 
-XCHG_COL_TO_ROW, XCHG_ROW_TO_COL, XCHG_COEFFS = 1, 2, 3
+XCHG_COL_TO_ROW, XCHG_ROW_TO_COL = 1, 2
+LAYOUT_HALO = 2      # mpfft_copy.dst_layout of a halo copy
 
 
 class MpfftError(RuntimeError):
@@ -113,17 +114,29 @@ def lib():
         h.mpfft_shard_stage_rows.restype = ctypes.c_int
         h.mpfft_shard_row_fused.argtypes = [_L, _L, _UL, _UL, ctypes.c_int]
         h.mpfft_shard_row_fused.restype = ctypes.c_int
-        h.mpfft_shard_combine_tmp_bytes.argtypes = [_L]
+        h.mpfft_shard_combine_tmp_bytes.argtypes = [_L, _L, _UL, _UL, ctypes.c_int]
         h.mpfft_shard_combine_tmp_bytes.restype = ctypes.c_size_t
-        h.mpfft_shard_combine.argtypes = [ctypes.POINTER(_Shard), ctypes.c_int, _vp, _L, _L, _L, _vp, ctypes.c_int,
-                                          _vp, ctypes.c_size_t, ctypes.c_int, _vp, _vp]
+        h.mpfft_shard_combine.argtypes = [ctypes.POINTER(_Shard), ctypes.c_int, _vp, _vp, _vp, _vp, _vp,
+                                          ctypes.c_size_t, _vp]
         h.mpfft_shard_combine.restype = ctypes.c_int
         _lp = ctypes.POINTER(ctypes.c_long)
-        h.mpfft_shard_partition.argtypes = [_L, _L, _UL, _UL, ctypes.c_int, _lp, _lp, _lp]
+        h.mpfft_shard_partition.argtypes = [_L, _L, _UL, _UL, ctypes.c_int, _lp, _lp]
         h.mpfft_shard_partition.restype = ctypes.c_int
+        h.mpfft_shard_stripes.argtypes = [_L, _L, _UL, _UL, ctypes.c_int, _lp, _L]
+        h.mpfft_shard_stripes.restype = ctypes.c_long
         h.mpfft_shard_exchange_plan.argtypes = [_L, _L, _UL, _UL, ctypes.c_int, ctypes.c_int,
                                                 ctypes.POINTER(_Copy), _L]
         h.mpfft_shard_exchange_plan.restype = ctypes.c_long
+        h.mpfft_shard_halo_plan.argtypes = [_L, _L, _UL, _UL, ctypes.c_int, ctypes.POINTER(_Copy), _L]
+        h.mpfft_shard_halo_plan.restype = ctypes.c_long
+        h.mpfft_shard_src_limbs.argtypes = [_L, _L, _UL, _UL, ctypes.c_int]
+        h.mpfft_shard_src_limbs.restype = ctypes.c_long
+        h.mpfft_shard_pack.argtypes = [_L, _L, _UL, _UL, ctypes.c_int, ctypes.c_int, _u64p, _L, _u64p]
+        h.mpfft_shard_pack.restype = ctypes.c_int
+        h.mpfft_mul_multi_device.argtypes = [_L, _L, _UL, _UL, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                             ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp),
+                                             ctypes.POINTER(_vp)]
+        h.mpfft_mul_multi_device.restype = ctypes.c_int
         h.mpfft_mul_multi.argtypes = [_u64p, _u64p, _L, _u64p, _L, _UL, _UL, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_int)]
         h.mpfft_mul_multi.restype = ctypes.c_int
@@ -411,13 +424,15 @@ def shard_stage_rows(which, desc, lo, hi, stream=None):
         raise MpfftError(rc, f"mpfft_shard_stage_rows({which}, {lo}, {hi})")
 
 
-def shard_combine_tmp_bytes(mcount):
-    return int(lib().mpfft_shard_combine_tmp_bytes(mcount))
+def shard_combine_tmp_bytes(n1, n2, depth, w, world):
+    return int(lib().mpfft_shard_combine_tmp_bytes(n1, n2, depth, w, world))
 
 
-def shard_combine(desc, phase, d_r, m0, mcount, kbase, halo, H, tmp, cin, d_sum, stream=None):
-    rc = lib().mpfft_shard_combine(ctypes.byref(desc), phase, _ptr(d_r), m0, mcount, kbase, _ptr(halo), H,
-                                   _ptr(tmp), tmp.numel(), cin, _ptr(d_sum), _stream(stream))
+def shard_combine(desc, phase, d_r, halo, d_sums, d_sums_all, tmp, stream=None):
+    """The rank's product stripes from its column layout (include/mpfft.h mpfft_shard_combine):
+    phase 0 with carry-in 0 + stripe summaries into d_sums, phase 1 the carries from d_sums_all."""
+    rc = lib().mpfft_shard_combine(ctypes.byref(desc), phase, _ptr(d_r), _ptr(halo), _ptr(d_sums), _ptr(d_sums_all),
+                                   _ptr(tmp), tmp.numel(), _stream(stream))
     if rc:
         raise MpfftError(rc, f"mpfft_shard_combine(phase {phase})")
 
@@ -425,28 +440,87 @@ def shard_combine(desc, phase, d_r, m0, mcount, kbase, halo, H, tmp, cin, d_sum,
 # ---- multi-GPU from one process (mpfft_mul_multi, multi.hip) ------------------------
 
 def shard_partition(n1, n2, depth, w, world):
-    """The C partition of one column-sharded multiply: dict rows, M (lists of world + 1),
-    C, chunk, H, Tr, fused (mpfft_shard_partition)."""
+    """The C partition of one column-sharded multiply: dict rows (list of world + 1), C, chunk,
+    H, Tr, fused, SL, S, ms (the stripes' first product limbs, S + 1) (mpfft_shard_partition,
+    mpfft_shard_stripes)."""
     rows = (ctypes.c_long * (world + 1))()
-    M = (ctypes.c_long * (world + 1))()
-    info = (ctypes.c_long * 5)()
-    rc = lib().mpfft_shard_partition(n1, n2, depth, w, world, rows, M, info)
+    info = (ctypes.c_long * 7)()
+    rc = lib().mpfft_shard_partition(n1, n2, depth, w, world, rows, info)
     if rc:
         raise MpfftError(rc, f"shard_partition(world={world})")
-    return {"rows": list(rows), "M": list(M), "C": info[0], "chunk": info[1], "H": info[2], "Tr": info[3],
-            "fused": bool(info[4])}
+    S = info[6]
+    ms = (ctypes.c_long * (S + 1))()
+    n = lib().mpfft_shard_stripes(n1, n2, depth, w, world, ms, S + 1)
+    if n != S + 1:
+        raise MpfftError(-n if n < 0 else 1, "shard_stripes")
+    return {"rows": list(rows), "C": info[0], "chunk": info[1], "H": info[2], "Tr": info[3],
+            "fused": bool(info[4]), "SL": info[5], "S": S, "ms": list(ms)}
+
+
+def _copies(fn, *args):
+    n = fn(*args, None, 0)
+    if n < 0:
+        raise MpfftError(-n, fn.__name__)
+    out = (_Copy * max(n, 1))()
+    n = fn(*args, out, n)
+    if n < 0:
+        raise MpfftError(-n, fn.__name__)
+    return [{f: getattr(out[i], f) for f, _ in _Copy._fields_} for i in range(n)]
 
 
 def shard_exchange_plan(n1, n2, depth, w, world, which):
     """The copies of exchange `which` (XCHG_*): list of dicts (mpfft_shard_exchange_plan)."""
-    n = lib().mpfft_shard_exchange_plan(n1, n2, depth, w, world, which, None, 0)
+    return _copies(lib().mpfft_shard_exchange_plan, n1, n2, depth, w, world, which)
+
+
+def shard_halo_plan(n1, n2, depth, w, world):
+    """The halo copies before the combine (mpfft_shard_halo_plan): column layout -> halo, limbs."""
+    return _copies(lib().mpfft_shard_halo_plan, n1, n2, depth, w, world)
+
+
+def shard_src_limbs(n1, n2, depth, w, world):
+    n = lib().mpfft_shard_src_limbs(n1, n2, depth, w, world)
     if n < 0:
-        raise MpfftError(-n, f"shard_exchange_plan(world={world}, which={which})")
-    out = (_Copy * max(n, 1))()
-    n = lib().mpfft_shard_exchange_plan(n1, n2, depth, w, world, which, out, n)
-    if n < 0:
-        raise MpfftError(-n, "shard_exchange_plan")
-    return [{f: getattr(out[i], f) for f, _ in _Copy._fields_} for i in range(n)]
+        raise MpfftError(-n, "shard_src_limbs")
+    return n
+
+
+def shard_pack(a, n1, n2, depth, w, world, rank):
+    """rank's operand slices of operand `a` (uint64 limbs), as the device-resident multi-GPU
+    entry and the sharded drivers read them (mpfft_shard_pack)."""
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    out = np.empty(shard_src_limbs(n1, n2, depth, w, world), dtype=np.uint64)
+    rc = lib().mpfft_shard_pack(n1, n2, depth, w, world, rank, _p(a), len(a), _p(out))
+    if rc:
+        raise MpfftError(rc, "shard_pack")
+    return out
+
+
+def mul_multi_device(n1, n2, depth, w, devices, src1, src2, outs, streams=None):
+    """Device-resident multi-GPU multiply (mpfft_mul_multi_device): src1[g], src2[g] rank g's
+    packed slices on devices[g] (torch tensors), outs[g] its Tr * SL stripe limbs.  streams:
+    torch streams per rank (the work is ordered on them), or None (returns when done)."""
+    G = len(devices)
+    devs = (ctypes.c_int * G)(*devices)
+    P = (_vp * G)
+    s1 = P(*[t.data_ptr() for t in src1])
+    s2 = P(*[t.data_ptr() for t in src2])
+    r = P(*[t.data_ptr() for t in outs])
+    st = P(*[s.cuda_stream for s in streams]) if streams is not None else None
+    rc = lib().mpfft_mul_multi_device(n1, n2, depth, w, G, devs, s1, s2, r, st)
+    if rc:
+        raise MpfftError(rc, f"mul_multi_device(devices={list(devices)})")
+
+
+def assemble_stripes(part, world, stripes):
+    """The product from every rank's stripe buffers (stripes[g]: Tr * SL limbs, uint64)."""
+    ms, SL = part["ms"], part["SL"]
+    out = np.empty(ms[-1], dtype=np.uint64)
+    for s in range(len(ms) - 1):
+        g, j = s % world, s // world
+        n = ms[s + 1] - ms[s]
+        out[ms[s]: ms[s + 1]] = stripes[g][j * SL: j * SL + n]
+    return out
 
 
 def mul_multi(i1, i2, depth, w, devices):

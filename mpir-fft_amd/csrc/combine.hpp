@@ -7,54 +7,40 @@
 // combine: r = sum_{k < len} c_k 2^(k bits1), c_k < 2^N canonical: per output limb the
 // 128-bit sum of the (at most a few) coefficient windows covering it, then the carry chain
 // by a decoupled look-back across blocks (k_combine1, one launch).
+//
+// Stripes.  The product is cut into S stripes of C coefficients: stripe s owns coefficients
+// [s C, (s+1) C) and product limbs [ms(s), ms(s+1)), ms(s) = min(total, floor(s C bits1 / 64)),
+// ms(S) = total.  A launch combines the stripes s = j G + g for j < nst (one rank's columns
+// of the column-sharded multiply: rank g of G holds C consecutive coefficients of every row
+// position j, so its stripes are exactly its column-layout rows -- mpfft_shard_combine).
+// Each stripe is its own carry chain with carry-in 0; its (generate, propagate) summary lets
+// the ranks' stripes be chained afterwards (k_stripe_carry).  The limbs of stripe s only
+// read coefficients below (s+1) C (64 ms(s+1) <= (s+1) C bits1), and the H coefficients
+// before s C come from `halo`.  The single-GPU combine is one stripe (G = S = 1) over the
+// whole coefficient array.
 // --------------------------------------------------------------------------
 struct CombArgs {
-    const u64 *dig;      // canonical coefficients c_k (< 2^N) in the (blocked) row layout
+    const u64 *dig;      // canonical coefficients: stripe j's C coefficients at dig + j C l
     int l;
     u64 N, bits1;
     long len;            // number of coefficients j1 + j2 - 1
-    long m0, mcount;     // output limbs [m0, m0 + mcount); the kernel also sums limb m0 - 1
-    long kbase;          // first locally stored coefficient (row r0 * NC)
-    const u64 *halo;     // coefficients [kbase - H, kbase) contiguous, or null
+    long total;          // product limbs
+    long C;              // coefficients per stripe
+    int G, g;            // stripe j of the launch is stripe j G + g of the product
+    long S;              // stripes of the product (the last one ends at limb `total`)
+    long bps;            // blocks per stripe
+    long SL;             // output stride: stripe j's limbs at r + j SL
+    const u64 *halo;     // stripe j's H coefficients before j G + g at halo + j H l (null: none needed)
     int H;
-    int NC, cbb, ccb;    // row layout: k -> p = k / NC - r0, c = k % NC,
-    long cbs;            //   slot = (c >> cbb) * cbs + p * ccb + (c & (ccb - 1))
-    long r0;
     double inv_bits1;    // 1.0 / bits1 (host), for the window bounds
 };
 
-// --------------------------------------------------------------------------
-// k_combine1<V>: the whole single-GPU combine in one launch.  Block b owns output limbs
-// [256 V b, 256 V (b+1)): it sums the coefficient windows of its limbs (coalesced,
-// limb m = base + k 256 + t), resolves its carries locally, and gets its carry-in by a
-// decoupled look-back over the blocks before it (flags in `st`, zeroed before the
-// launch).  b is a ticket from an atomic counter (st[nblocks]), not blockIdx.x: a block
-// only ever waits on blocks that took a smaller ticket, i.e. that are already running,
-// whatever order the hardware dispatches workgroups in.
-// The flag is the whole message (no data published beside it), so relaxed agent-scope
-// atomics suffice: release/acquire would write back / invalidate the XCD's L2 per block.
-// Block flag: 0 not ready, 1 aggregate generates, 2 aggregate propagates, 3 aggregate
-// kills, 4 / 5 inclusive carry-out 0 / 1.
-// --------------------------------------------------------------------------
-// limbs per block: 256 V (host: comb_v())
-
-// floor(x / d) for x < 2^52: double quotient, then an exact integer fix-up
-__device__ __forceinline__ long udiv_exact(u64 x, u64 d)
+// first product limb of stripe s
+__device__ __forceinline__ long stripe_m(const CombArgs &a, long s)
 {
-    long q = (long)((double)x / (double)d);
-    while ((u64)q * d > x) --q;
-    while ((u64)(q + 1) * d <= x) ++q;
-    return q;
-}
-
-// coef_ptr for a power-of-two NC (always: NC = 2^floor(depth/2)) and no halo
-__device__ __forceinline__ const u64 *coef_ptr2(const CombArgs &a, long k)
-{
-    const int lg = __builtin_ctz((unsigned)a.NC);
-    const long p = (k >> lg) - a.r0;
-    const int cc = (int)(k & (a.NC - 1));
-    const long slot = (long)(cc >> a.cbb) * a.cbs + p * a.ccb + (cc & (a.ccb - 1));
-    return a.dig + (size_t)slot * a.l;
+    if (s >= a.S) return a.total;
+    const long m = (long)(((u64)s * (u64)a.C * a.bits1) >> 6);
+    return m < a.total ? m : a.total;
 }
 
 // floor(x / d) for x < 2^52 from a precomputed inv = fl(1/d): the double product is within
@@ -67,13 +53,19 @@ __device__ __forceinline__ long udiv_inv(u64 x, u64 d, double inv)
     return q;
 }
 
-// m: global product limb (a.m0 + local index); coefficients below kbase come from the halo
-// (a rank's combine in the sharded multiply), the rest from the row layout.
-// KM > 0: at most KM coefficients cover a limb (host: ceil((N + 63) / bits1) <= KM), a
-// fixed-trip loop of guarded loads, so a thread's loads for all its limbs can be in flight
-// together (the combine is latency-bound otherwise); KM = 0: any count.
+// one stripe's view: its coefficients from kbase on at cdig + (k - kbase) l, the H before it
+// at chalo + (k - kbase + H) l
+struct StripeView {
+    const u64 *cdig, *chalo;
+    long kbase;
+};
+
+// m: global product limb.  KM > 0: at most KM coefficients cover a limb (host:
+// ceil((N + 63) / bits1) <= KM), a fixed-trip loop of guarded loads, so a thread's loads for
+// all its limbs can be in flight together (the combine is latency-bound otherwise); KM = 0:
+// any count.
 template <int KM>
-__device__ __forceinline__ void comb_limb(const CombArgs &a, long m, u64 *lo, u32 *hi)
+__device__ __forceinline__ void comb_limb(const CombArgs &a, const StripeView &sv, long m, u64 *lo, u32 *hi)
 {
     const u64 P = (u64)m * 64;
     // first coefficient reaching past bit P (k bits1 + N > P) .. last starting below P + 64
@@ -89,7 +81,8 @@ __device__ __forceinline__ void comb_limb(const CombArgs &a, long m, u64 *lo, u3
         const u64 o = P + 64 - st;
         const long q = (long)(o >> 6) - 1;
         const int sb = (int)(o & 63);
-        const u64 *cp = k < a.kbase ? a.halo + (size_t)(k - (a.kbase - a.H)) * a.l : coef_ptr2(a, k);
+        const long d = k - sv.kbase;
+        const u64 *cp = d < 0 ? sv.chalo + (d + a.H) * (long)a.l : sv.cdig + d * (long)a.l;
         const u64 w0 = (in && q >= 0 && q < a.l) ? cp[q] : 0;
         const u64 w1 = (in && sb && q + 1 < a.l) ? cp[q + 1] : 0;
         const u64 v = sb ? (w0 >> sb) | (w1 << (64 - sb)) : w0;
@@ -107,10 +100,22 @@ __device__ __forceinline__ void comb_limb(const CombArgs &a, long m, u64 *lo, u3
     *hi = shi;
 }
 
-// r[i] = product limb a.m0 + i for i < a.mcount.  A rank of the sharded multiply (m0 > 0)
-// starts from carry-in 0 and the overflow of limb m0 - 1; its carry-out with that carry-in
-// ends in st[nblocks - 1] (4 + carry) and, when `allp` is given, allp[b] = 1 for every block
-// whose limbs all propagate (k_comb_summary turns both into the rank's (generate, propagate)).
+// --------------------------------------------------------------------------
+// k_combine1<V, KM>: nst stripes in one launch, bps blocks of 256 V limbs each.  Block
+// (j, b) owns limbs [256 V b, 256 V (b+1)) of stripe j: it sums their coefficient windows
+// (coalesced, limb base + k 256 + t), resolves its carries locally, and gets its carry-in by
+// a decoupled look-back over the blocks of its stripe before it (flags in `st`, zeroed
+// before the launch).  The block index is a ticket from an atomic counter (st[nst bps]), not
+// blockIdx.x: a block only ever waits on blocks that took a smaller ticket, i.e. that are
+// already running, whatever order the hardware dispatches workgroups in.
+// The flag is the whole message (no data published beside it), so relaxed agent-scope
+// atomics suffice: release/acquire would write back / invalidate the XCD's L2 per block.
+// Block flag: 0 not ready, 1 aggregate generates, 2 aggregate propagates, 3 aggregate
+// kills, 4 / 5 inclusive carry-out 0 / 1 (every flag ends at 4 or 5).  Limbs past the
+// stripe's end are transparent (propagate), so a stripe's last flag is its carry-out; the
+// overflow of its last limb's window sum belongs to the next stripe (its limb ms - 1).
+// allp_out (or null): per block, 1 if all its limbs propagate (k_comb_summary).
+// --------------------------------------------------------------------------
 template <int CB_V, int KM>
 __global__ __launch_bounds__(256) void k_combine1(CombArgs a, u64 *r, u32 *st, u32 *allp_out)
 {
@@ -120,10 +125,17 @@ __global__ __launch_bounds__(256) void k_combine1(CombArgs a, u64 *r, u32 *st, u
     __shared__ u64 scr[64];
     __shared__ u32 sh_cin, sh_b;
     const WG c = wg_ctx();
-    const long total = a.mcount;
     if (c.t == 0) sh_b = __hip_atomic_fetch_add(&st[gridDim.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    const long b = sh_b;   // ticket: every block below b has started
+    const long tk = sh_b;        // ticket: every block below it has started
+    const long j = tk / a.bps, b = tk - j * a.bps;
+    const long s = j * a.G + a.g;
+    const long m0 = stripe_m(a, s);
+    const long total = stripe_m(a, s + 1) - m0;
+    StripeView sv;
+    sv.kbase = s * a.C;
+    sv.cdig = a.dig + j * a.C * (long)a.l;
+    sv.chalo = a.halo ? a.halo + j * (long)a.H * a.l : nullptr;
     const long base = b * CB_LIMBS;
     // window sums: lo of limb base + i -> L[i], its carry (hi) -> H[i + 1]
 #pragma unroll
@@ -132,14 +144,14 @@ __global__ __launch_bounds__(256) void k_combine1(CombArgs a, u64 *r, u32 *st, u
         const long m = base + i;
         u64 lo = 0;
         u32 hi = 0;
-        if (m < total) comb_limb<KM>(a, a.m0 + m, &lo, &hi);
+        if (m < total) comb_limb<KM>(a, sv, m0 + m, &lo, &hi);
         L[i] = lo;
         H[i + 1] = hi;
     }
     if (c.t == 0) {
         u64 lo = 0;
         u32 hi = 0;
-        if (a.m0 + base > 0) comb_limb<KM>(a, a.m0 + base - 1, &lo, &hi);
+        if (m0 + base > 0 && base < total) comb_limb<KM>(a, sv, m0 + base - 1, &lo, &hi);
         H[0] = hi;
     }
     __syncthreads();
@@ -150,8 +162,9 @@ __global__ __launch_bounds__(256) void k_combine1(CombArgs a, u64 *r, u32 *st, u
 #pragma unroll
     for (int k = 0; k < CB_V; ++k) {
         const int i = c.t * CB_V + k;
-        const bool gk = add_ovf(L[i], (u64)H[i], &v[k]);
-        const bool pk = v[k] == MPF_MAXL;
+        const bool real = base + i < total;
+        const bool gk = add_ovf(L[i], (u64)H[i], &v[k]) && real;
+        const bool pk = v[k] == MPF_MAXL || !real;
         g |= (u32)gk << k;
         p |= (u32)pk << k;
         G = gk || (pk && G);
@@ -160,25 +173,26 @@ __global__ __launch_bounds__(256) void k_combine1(CombArgs a, u64 *r, u32 *st, u
     u32 co0;
     wg_scan<1>(c, G, Pa, 0, &co0, scr);
     const bool allp = __syncthreads_and(Pa);
-    if (allp_out && c.t == 0) allp_out[b] = allp ? 1u : 0u;
+    u32 *fl = st + j * a.bps;    // this stripe's flags
+    if (allp_out && c.t == 0) allp_out[tk] = allp ? 1u : 0u;
     // look-back (thread 0)
     if (c.t == 0) {
         u32 cin = 0;
         if (b == 0) {
-            __hip_atomic_store(&st[0], 4u + co0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&fl[0], 4u + co0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             const u32 agg = co0 ? 1u : (allp ? 2u : 3u);
-            if (agg != 2u) __hip_atomic_store(&st[b], agg == 1u ? 5u : 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else __hip_atomic_store(&st[b], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (long j = b - 1;; --j) {
+            if (agg != 2u) __hip_atomic_store(&fl[b], agg == 1u ? 5u : 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else __hip_atomic_store(&fl[b], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (long q = b - 1;; --q) {
                 u32 f;
-                while ((f = __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u)
+                while ((f = __hip_atomic_load(&fl[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u)
                     __builtin_amdgcn_s_sleep(1);
                 if (f >= 4u) { cin = f - 4u; break; }
                 if (f == 1u) { cin = 1; break; }
                 if (f == 3u) { cin = 0; break; }
             }
-            if (agg == 2u) __hip_atomic_store(&st[b], 4u + cin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (agg == 2u) __hip_atomic_store(&fl[b], 4u + cin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         sh_cin = cin;
     }
@@ -192,46 +206,79 @@ __global__ __launch_bounds__(256) void k_combine1(CombArgs a, u64 *r, u32 *st, u
         run = ((g >> k) & 1) || (((p >> k) & 1) && run);
     }
     __syncthreads();
+    u64 *rs = r + j * a.SL;
 #pragma unroll
     for (int k = 0; k < CB_V; ++k) {
         const long m = base + k * 256 + c.t;
-        if (m < total) r[m] = L[k * 256 + c.t];
+        if (m < total) rs[m] = L[k * 256 + c.t];
     }
 }
 
-// rank summary of a k_combine1 launch over nb blocks: sum[0] = carry out with carry-in 0
-// (the last block's resolved flag), sum[1] = every limb propagates (all-ones)
-__global__ __launch_bounds__(256) void k_comb_summary(const u32 *st, const u32 *allp, long nb, int *sum)
+// stripe summaries of a k_combine1 launch (one workgroup per stripe j, bps blocks each):
+// sum[2 j] = carry out with carry-in 0 (the stripe's last flag), sum[2 j + 1] = every limb
+// propagates (all-ones)
+__global__ __launch_bounds__(256) void k_comb_summary(const u32 *st, const u32 *allp, long bps, int *sum)
 {
     __shared__ int all;
+    const long j = blockIdx.x;
     if (threadIdx.x == 0) all = 1;
     __syncthreads();
     int mine = 1;
-    for (long b = threadIdx.x; b < nb; b += blockDim.x) mine &= allp[b] ? 1 : 0;
+    for (long b = threadIdx.x; b < bps; b += blockDim.x) mine &= allp[j * bps + b] ? 1 : 0;
     if (!mine) all = 0;
     __syncthreads();
     if (threadIdx.x == 0) {
-        sum[0] = (int)(st[nb - 1] - 4u);
-        sum[1] = all;
+        sum[2 * j] = (int)(st[j * bps + bps - 1] - 4u);
+        sum[2 * j + 1] = all;
     }
 }
 
-// r[0 .. n) += 1 (the carry into a rank's limb range from the ranks below): one workgroup
-// walks 256-limb chunks until the first limb that is not all-ones (the first, almost always)
-__global__ __launch_bounds__(256) void k_carry_in(u64 *r, long n)
+// --------------------------------------------------------------------------
+// k_stripe_carry: the carries between stripes.  sums = the G ranks' k_comb_summary outputs
+// in rank order ([rank][j][2], nst stripes each): workgroup j finds the carry into stripe
+// s = j G + g -- the (generate, propagate) chain of stripes 0 .. s-1 in product order, each
+// thread composing a contiguous run of them, thread 0 chaining the runs -- and, when it is
+// 1, adds it to the stripe's limbs (r + j SL, `stripe_m` bounds): every all-ones limb wraps to
+// zero up to the first one that does not (almost always the first).
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_stripe_carry(CombArgs a, long nst, const int *sums, u64 *r)
 {
-    __shared__ int stop;
+    __shared__ u32 gs[256], ps[256];
+    __shared__ int cin_sh, stop;
+    const long j = blockIdx.x;
+    const long s = j * a.G + a.g;
+    const int t = threadIdx.x;
+    const long per = (s + 255) / 256;
+    u32 G = 0, P = 1;
+    for (long q = t * per; q < s && q < (t + 1) * per; ++q) {   // stripes q in product order
+        const long e = (q % a.G) * nst + q / a.G;
+        const u32 gq = (u32)sums[2 * e], pq = (u32)sums[2 * e + 1];
+        G = gq | (pq & G);
+        P &= pq;
+    }
+    gs[t] = G;
+    ps[t] = P;
+    __syncthreads();
+    if (t == 0) {
+        u32 cin = 0;
+        for (int u = 0; u < 256; ++u) cin = gs[u] | (ps[u] & cin);
+        cin_sh = (int)cin;
+    }
+    __syncthreads();
+    if (!cin_sh) return;
+    const long m0 = stripe_m(a, s), n = stripe_m(a, s + 1) - m0;
+    u64 *rs = r + j * a.SL;
     for (long c0 = 0; c0 < n; c0 += 256) {
-        const long m = c0 + threadIdx.x;
-        const bool ones = m < n && r[m] == MPF_MAXL;
+        const long m = c0 + t;
+        const bool ones = m < n && rs[m] == MPF_MAXL;
         const u64 nz = __ballot(!ones && m < n);
-        if (threadIdx.x == 0) stop = 1 << 30;
+        if (t == 0) stop = 1 << 30;
         __syncthreads();
-        if ((threadIdx.x & 63) == 0 && nz) atomicMin(&stop, (int)(threadIdx.x + __builtin_ctzll(nz)));
+        if ((t & 63) == 0 && nz) atomicMin(&stop, (int)(t + __builtin_ctzll(nz)));
         __syncthreads();
         const int first = stop;   // first non-all-ones limb of this chunk (or none)
-        if (m < n && (int)threadIdx.x < first) r[m] = 0;          // all-ones limbs wrap to zero
-        if (m < n && (int)threadIdx.x == first) r[m] += 1;
+        if (m < n && t < first) rs[m] = 0;          // all-ones limbs wrap to zero
+        if (m < n && t == first) rs[m] += 1;
         if (first < 256) return;
         __syncthreads();
     }

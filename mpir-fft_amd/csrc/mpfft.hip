@@ -85,7 +85,7 @@ struct Plan {
     bool sqrt2;         // new_mpn_mul6 plan: 4n slots, bits1 = (N - depth - 1)/2, Tr up to 2 NR
     size_t slots;       // allocated slots per operand
     // off_flags: k_combine1's look-back flags + ticket counter, cleared by the first forward
-    // look-back flags + ticket counter, cleared by the first forward column pass
+    // column pass
     // (Exec::zflags) -- no stage between that pass and the combine may use this region
     size_t off_digA, off_topA, off_cbA, off_digB, off_topB, off_cbB, off_flags, bytes;
     bool has_c;         // a third coefficient array C: the fused pointwise (k_pwss PAIR) writes there
@@ -1170,33 +1170,22 @@ struct Exec {
         return MPFFT_OK;
     }
 
-    // combine the canonical coefficients of the row layout (A) into product limbs
-    // [m0, m0 + mcount) of r (r[0] = limb m0) in one k_combine1 launch: window sums plus a
-    // decoupled look-back carry chain, carry-in 0.  `kbase` is the first coefficient of the
-    // row layout, `halo` the H coefficients before it (a rank of the sharded multiply).
-    // st: the look-back flags (comb_flag_words(mcount) u32, zeroed here unless `cleared`);
-    // allp (or null): per-block all-ones flags for the rank summary.
-    int combine1(u64 *r, long m0, long mcount, long kbase, const u64 *halo, int H, u32 *st, bool cleared, u32 *allp)
+    // combine stripes (combine.hpp): `a` names the coefficients, the stripes (a.G, a.g, a.S, a.C)
+    // and the halo; nst stripes of this launch, each comb_blocks(stripe limbs) blocks, in one
+    // k_combine1 launch (window sums plus a per-stripe decoupled look-back carry chain, carry-in
+    // 0).  st: the look-back flags (nst bps + 1 u32, zeroed here unless `cleared`); allp (or
+    // null): per-block all-ones flags for the stripe summaries.
+    int combine1(CombArgs a, long nst, long stripe_limbs, u64 *r, u32 *st, bool cleared, u32 *allp)
     {
-        CombArgs a;
-        a.dig = row.dig[0];
         a.l = (int)P.l;
         a.N = P.N;
         a.bits1 = P.bits1;
         a.len = P.len;
-        a.m0 = m0;
-        a.mcount = mcount;
-        a.kbase = kbase;
-        a.halo = halo;
-        a.H = H;
-        a.NC = (int)P.NC;
-        a.cbb = cbb;
-        a.ccb = ccb;
-        a.cbs = cbs;
-        a.r0 = r0;
+        a.total = P.total;
         a.inv_bits1 = 1.0 / (double)P.bits1;
-        const long nb = comb_blocks(mcount);
-        if (!cleared) HIPCHK(hipMemsetAsync(st, 0, (size_t)comb_flag_words(mcount) * 4, s));   // one fill
+        a.bps = comb_blocks(stripe_limbs);
+        const long nb = nst * a.bps;
+        if (!cleared) HIPCHK(hipMemsetAsync(st, 0, (size_t)(nb + 1) * 4, s));   // one fill
         const int v = comb_v();
         const bool k3 = (P.N + 63 + P.bits1 - 1) / P.bits1 <= 3;   // at most 3 coefficients cover a limb
         void (*f)(CombArgs, u64 *, u32 *, u32 *) =
@@ -1209,10 +1198,17 @@ struct Exec {
         return MPFFT_OK;
     }
 
+    // one GPU: a single stripe over the natural slot order (coefficient k at slot k)
     int combine_single(u64 *r, unsigned char *ws)
     {
         u32 *st = comb_flags(ws);
-        return combine1(r, 0, P.total, 0, nullptr, 0, st, zflags == st, nullptr);
+        CombArgs a;
+        memset(&a, 0, sizeof(a));
+        a.dig = row.dig[0];
+        a.C = P.trunc;
+        a.G = 1;
+        a.S = 1;
+        return combine1(a, 1, P.total, r, st, zflags == st, nullptr);
     }
 };
 
@@ -1673,39 +1669,72 @@ int mpfft_shard_stage(int stage, const mpfft_shard *sh, const uint64_t *d_i1, co
     return MPFFT_EINVAL;
 }
 
-size_t mpfft_shard_combine_tmp_bytes(long mcount)
+// the stripes of one rank of the column-sharded multiply (multi.hip mpfft_shard_partition):
+// stripe j of rank g (g = c0 / ccount of G = NC / ccount ranks) is product stripe j G + g,
+// coefficients [(j G + g) C, + C) = column-layout row j of the rank
+static void shard_comb_args(const Plan &P, const mpfft_shard *sh, CombArgs *a, long *nst, long *stripe_limbs)
 {
-    if (mcount < 1) return 0;
-    return align_up((size_t)Exec::comb_flag_words(mcount) * 4, 256) + align_up((size_t)Exec::comb_blocks(mcount) * 4, 256);
+    memset(a, 0, sizeof(*a));
+    a->C = sh->ccount;
+    a->G = (int)(P.NC / sh->ccount);
+    a->g = sh->c0 / sh->ccount;
+    a->S = (long)a->G * P.Tr;
+    *nst = P.Tr;
+    // limbs of a stripe at most: ms(s+1) - ms(s) <= ceil(C bits1 / 64); the last stripe runs to
+    // the product's end, 64 total <= (len + 1) bits1 <= (T + 1) bits1: at most (C + 1) bits1 / 64 + 2
+    *stripe_limbs = (long)((((u64)sh->ccount + 1) * P.bits1) / 64) + 2;
 }
 
-int mpfft_shard_combine(const mpfft_shard *sh, int phase, uint64_t *d_r, long m0, long mcount, long kbase,
-                        const uint64_t *halo, int H, void *d_tmp, size_t tmp_bytes, int cin, int *d_sum,
-                        void *stream)
+size_t mpfft_shard_combine_tmp_bytes(long n1, long n2, unsigned long depth, unsigned long w, int world)
+{
+    Plan P;
+    if (make_plan(&P, n1, n2, depth, w) || world < 1 || P.NC % world) return 0;
+    const long sl = (long)((((u64)(P.NC / world) + 1) * P.bits1) / 64) + 2;
+    const long nb = P.Tr * Exec::comb_blocks(sl);
+    return align_up((size_t)(nb + 1) * 4, 256) + align_up((size_t)nb * 4, 256);
+}
+
+int mpfft_shard_combine(const mpfft_shard *sh, int phase, uint64_t *d_r, const uint64_t *d_halo, int *d_sums,
+                        const int *d_sums_all, void *d_tmp, size_t tmp_bytes, void *stream)
 {
     Plan P;
     int rc = make_plan(&P, sh->n1, sh->n2, sh->depth, sh->w);
     if (rc) return rc;
-    if (mcount < 1 || m0 < 0 || m0 + mcount > P.total) return MPFFT_EINVAL;
-    if (tmp_bytes < mpfft_shard_combine_tmp_bytes(mcount)) return MPFFT_ENOMEM;
-    if (phase == 0 && (!d_sum || (kbase > 0 && (!halo || H < 1)))) return MPFFT_EINVAL;
+    if (sh->ccount < 1 || P.NC % sh->ccount || sh->c0 % sh->ccount) return MPFFT_EINVAL;
+    const int world = (int)(P.NC / sh->ccount);
+    if (tmp_bytes < mpfft_shard_combine_tmp_bytes(sh->n1, sh->n2, sh->depth, sh->w, world)) return MPFFT_ENOMEM;
+    const long H = (long)((P.N + 128 + P.bits1 - 1) / P.bits1) + 1;
+    if (phase == 0 && (!d_sums || (!d_halo && (long)world * P.Tr > 1))) return MPFFT_EINVAL;
+    if (phase == 1 && !d_sums_all) return MPFFT_EINVAL;
     (void)hipGetLastError();
     Exec X(P, (hipStream_t)stream);
     if ((rc = shard_exec(X, sh))) return rc;
+    CombArgs a;
+    long nst, sl;
+    shard_comb_args(P, sh, &a, &nst, &sl);
+    a.dig = X.col.dig[0];
+    a.halo = d_halo;
+    a.H = (int)H;
+    a.SL = sl;
+    const long nb = nst * Exec::comb_blocks(sl);
     u32 *st = (u32 *)d_tmp;
-    u32 *allp = (u32 *)((unsigned char *)d_tmp + align_up((size_t)Exec::comb_flag_words(mcount) * 4, 256));
+    u32 *allp = (u32 *)((unsigned char *)d_tmp + align_up((size_t)(nb + 1) * 4, 256));
     hipStream_t s = (hipStream_t)stream;
-    if (phase == 0) {   // the rank's limbs with carry-in 0, and its (generate, propagate) summary
-        if ((rc = X.combine1(d_r, m0, mcount, kbase, halo, H, st, false, allp))) return rc;
-        hipLaunchKernelGGL(k_comb_summary, dim3(1), dim3(256), 0, s, (const u32 *)st, (const u32 *)allp,
-                           Exec::comb_blocks(mcount), d_sum);
+    if (phase == 0) {   // every stripe with carry-in 0, and its (generate, propagate) summary
+        if ((rc = X.combine1(a, nst, sl, d_r, st, false, allp))) return rc;
+        hipLaunchKernelGGL(k_comb_summary, dim3((unsigned)nst), dim3(256), 0, s, (const u32 *)st, (const u32 *)allp,
+                           Exec::comb_blocks(sl), d_sums);
         HIPCHK(hipGetLastError());
         return MPFFT_OK;
     }
-    if (cin) {          // the carry from the ranks below: +1 over the run of all-ones limbs
-        hipLaunchKernelGGL(k_carry_in, dim3(1), dim3(256), 0, s, d_r, mcount);
-        HIPCHK(hipGetLastError());
-    }
+    // the carries between stripes, from every rank's summaries
+    a.l = (int)P.l;
+    a.N = P.N;
+    a.bits1 = P.bits1;
+    a.len = P.len;
+    a.total = P.total;
+    hipLaunchKernelGGL(k_stripe_carry, dim3((unsigned)nst), dim3(256), 0, s, a, nst, d_sums_all, d_r);
+    HIPCHK(hipGetLastError());
     return MPFFT_OK;
 }
 
@@ -1777,7 +1806,9 @@ int mpfft_mul_ex(uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i2, 
     std::vector<int> devs;
     if (mpfft_multi_policy(n1, n2, depth, w, devs) > 1) {   // column-sharded over the policy's devices
         g_last_ngpus = (int)devs.size();
-        return mpfft_mul_multi(r1, i1, n1, i2, n2, depth, w, (int)devs.size(), devs.data());
+        rc = mpfft_mul_multi(r1, i1, n1, i2, n2, depth, w, (int)devs.size(), devs.data());
+        // the policy's devices missing or full: the product still fits one device
+        if (rc != MPFFT_ENODEV && rc != MPFFT_ENOMEM) return rc;
     }
     g_last_ngpus = 1;
     return mul_host(P, r1, i1, n1, i2, n2);

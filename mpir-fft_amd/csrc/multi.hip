@@ -14,9 +14,16 @@
 //   stage     forward rows, pointwise, inverse rows
 //   xchg #2   row layout -> column layout, the product
 //   stage     truncated inverse columns + scale
-//   xchg #3   canonical coefficients -> contiguous ranges; H halo coefficients from rank g-1
-//   combine   phase 0 (carry-in 0) per rank, the cross-rank carry on the host, phase 1
-//   D2H       rank g's product limbs [M_g, M_g+1) (one thread per rank)
+//   halo      the H coefficients before each of the rank's stripes (a few per row position)
+//   combine   in the column layout: rank g's C columns of row position j are product stripe
+//             j G + g (C consecutive coefficients, a contiguous bit range), combined with
+//             carry-in 0 (phase 0); every rank's stripe summaries to every rank (peer copies of
+//             Tr (generate, propagate) pairs); phase 1 adds each stripe's carry-in on the device
+//   D2H       rank g's stripes into their places in r1 (one thread per rank)
+//
+// The product never moves back to row owners: the combine needs only each stripe's few halo
+// coefficients (the reference's TODO:53-59, "combine just a single coefficient at a time so
+// that cache locality can be maintained for the MFA IFFT's").
 //
 // Every rank's work is queued on its own stream; an exchange's copies run on the receiving
 // rank's stream after it waited for the senders' events (pull), so no host barrier sits
@@ -28,6 +35,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -42,16 +50,28 @@ namespace {
 
 struct Part {
     int world;
+    unsigned long depth, w;
     long n1, n2, total, n, l, NC, NR, T, Tr, bits1, N, len;
     long C, chunk, H, cbw;
+    long S, SL;    // product stripes (world Tr) and the most limbs of one (the combine's d_r stride)
     bool fused;
     bool rep;      // replicated forward columns: every rank computes every column block (world 2)
     long nsl() const { return rep ? world : 1; }   // operand column slices a rank holds
-    std::vector<long> rows, M;
+    long src_limbs() const { return nsl() * Tr * chunk; }
+    std::vector<long> rows, ms;   // ms[s]: first product limb of stripe s (combine.hpp stripe_m)
     long rcount(int d) const { return rows[d + 1] - rows[d]; }
 };
 
 long cb_words_l(long l) { return 2 * ((l + 63) / 64); }
+
+// replicated forward columns at two ranks (sharded.py ShardedMul.replicates: exchange #1 there
+// is one xGMI link carrying the other rank's rows of both column blocks; the second column
+// block is one more column phase of HBM-bound passes); MPFFT_REPLICATE_COLUMNS=0/1 overrides
+bool replicated(int world)
+{
+    const char *e = getenv("MPFFT_REPLICATE_COLUMNS");
+    return e ? (e[0] == '1' && world > 1) : world == 2;
+}
 
 // ShardPlan (sharded.py) in C: the same arithmetic, so both drivers agree slot for slot
 int partition(Part &p, long n1, long n2, unsigned long depth, unsigned long w, int world)
@@ -60,6 +80,8 @@ int partition(Part &p, long n1, long n2, unsigned long depth, unsigned long w, i
     int rc = mpfft_plan_info(n1, n2, depth, w, info);
     if (rc) return rc;
     p.world = world;
+    p.depth = depth;
+    p.w = w;
     p.n1 = n1;
     p.n2 = n2;
     p.total = n1 + n2;
@@ -76,32 +98,32 @@ int partition(Part &p, long n1, long n2, unsigned long depth, unsigned long w, i
     p.C = p.NC / world;
     p.rows.assign(world + 1, 0);
     for (int d = 0; d <= world; ++d) p.rows[d] = ((long)d * p.Tr) / world;
-    p.M.assign(world + 1, 0);
-    for (int d = 1; d < world; ++d) {
-        const long m = (long)(((unsigned __int128)(p.rows[d] * p.NC) * (u64)p.bits1) / 64);
-        p.M[d] = m < p.total ? m : p.total;
-    }
-    p.M[world] = p.total;
+    if (p.Tr < world) return MPFFT_EINVAL;
+    for (int d = 0; d < world; ++d)
+        if (p.rows[d + 1] - p.rows[d] < 1) return MPFFT_EINVAL;  // a rank without rows
     p.H = (p.N + 128 + p.bits1 - 1) / p.bits1 + 1;
     p.cbw = cb_words_l(p.l);
-    for (int d = 1; d < world; ++d) {
-        if (p.rows[d] * p.NC < p.H) return MPFFT_EINVAL;       // the halo would span ranks
-        if (p.rows[d + 1] - p.rows[d] < 1) return MPFFT_EINVAL;  // a rank without rows
-    }
-    if (p.Tr < world) return MPFFT_EINVAL;
     p.chunk = (p.C * p.bits1 + 63) / 64 + 2;
     p.fused = mpfft_shard_row_fused(n1, n2, depth, w, (int)p.C) != 0;
-    p.rep = false;
+    p.rep = replicated(world);
+    p.S = (long)world * p.Tr;
+    p.SL = (long)((((u64)p.C + 1) * (u64)p.bits1) / 64) + 2;   // mpfft.hip shard_comb_args
+    p.ms.assign(p.S + 1, p.total);
+    for (long s = 0; s < p.S; ++s) {
+        const long m = (long)(((u64)s * (u64)p.C * (u64)p.bits1) >> 6);
+        p.ms[s] = m < p.total ? m : p.total;
+    }
     return MPFFT_OK;
 }
 
 long field_width(const Part &p, int f) { return f == 0 ? p.l : f == 1 ? p.cbw : 1; }
 
-// the copies of one exchange (sharded.py ShardedMul._col_to_row / _row_to_col)
+// the copies of one exchange (sharded.py ShardedMul._exchange): #1 column layout rows
+// [rows[d], rows[d+1]) -> rank d's row layout (both operands), #2 the product back
 void exchange_plan(const Part &p, int which, std::vector<mpfft_copy> &out)
 {
     out.clear();
-    const int nf = which == MPFFT_XCHG_COEFFS ? 1 : 3;
+    const int nf = 3;
     const int nop = which == MPFFT_XCHG_COL_TO_ROW ? 2 : 1;
     for (int d = 0; d < p.world; ++d)          // row-layout rank (receiver of #1/#3, sender of #2)
         for (int s = 0; s < p.world; ++s)      // column-layout rank
@@ -118,6 +140,106 @@ void exchange_plan(const Part &p, int which, std::vector<mpfft_copy> &out)
                     }
                     if (cnt) out.push_back(c);
                 }
+}
+
+// the halo copies (sharded.py ShardedMul._halo): for stripe s = j G + g, coefficients
+// [s C - H, s C) from the ranks holding them (stripe t = k / C: rank t % G, column-layout
+// slot (t / G) C + k % C) to rank g's halo slot j H + k - (s C - H), split into runs of one
+// source stripe; offsets and counts in limbs
+void halo_plan(const Part &p, std::vector<mpfft_copy> &out)
+{
+    out.clear();
+    for (int g = 0; g < p.world; ++g)
+        for (long j = 0; j < p.Tr; ++j) {
+            const long s = j * p.world + g, k1 = s * p.C, k0 = k1 - p.H;
+            for (long k = k0 > 0 ? k0 : 0; k < k1;) {
+                const long t = k / p.C, ke = (t + 1) * p.C < k1 ? (t + 1) * p.C : k1;
+                const long src_slot = (t / p.world) * p.C + k % p.C, dst_slot = j * p.H + (k - k0);
+                mpfft_copy c = {(int)(t % p.world), g, 0, 0, 0, MPFFT_LAYOUT_HALO, src_slot * p.l, dst_slot * p.l,
+                                (ke - k) * p.l};
+                out.push_back(c);
+                k = ke;
+            }
+        }
+}
+
+// A run of limbs copied by k_copy_runs: src offset -> dst offset, n limbs
+struct Run {
+    long src, dst, n;
+};
+
+// one workgroup per run (grid-stride): the halo's pack on the sender (column layout -> one
+// contiguous block per receiver) and, where a receiver's runs from one sender are not
+// contiguous in its halo, the scatter from its staging buffer
+__global__ __launch_bounds__(256) void k_copy_runs(const Run *runs, long nruns, const u64 *src, u64 *dst)
+{
+    for (long r = blockIdx.x; r < nruns; r += gridDim.x) {
+        const Run R = runs[r];
+        for (long i = threadIdx.x; i < R.n; i += blockDim.x) dst[R.dst + i] = src[R.src + i];
+    }
+}
+
+// the halo plan as transfers: per sender one pack launch into its send block (grouped by
+// receiver), one peer copy per (sender, receiver) pair -- straight into the receiver's halo
+// when that sender's runs are contiguous there (always when H <= C: stripe j G + g's halo is
+// the tail of stripe j G + g - 1), else into a staging block the receiver scatters
+struct HaloRank {
+    std::vector<Run> pack, scatter;
+    long send_n = 0, stage_n = 0;
+    std::vector<long> send_off, send_cnt;   // per receiver: its block of the send buffer
+    std::vector<long> recv_halo;            // per sender: halo offset of its block, or -1: staging
+    std::vector<long> recv_stage;           // per sender: staging offset of its block
+};
+
+void halo_xfer(const Part &p, std::vector<HaloRank> &hr)
+{
+    std::vector<mpfft_copy> plan;
+    halo_plan(p, plan);
+    const int G = p.world;
+    hr.assign(G, HaloRank());
+    for (int s = 0; s < G; ++s) {
+        HaloRank &S = hr[s];
+        S.send_off.assign(G, 0);
+        S.send_cnt.assign(G, 0);
+        for (int d = 0; d < G; ++d) {
+            S.send_off[d] = S.send_n;
+            for (const mpfft_copy &c : plan)
+                if (c.src == s && c.dst == d) {
+                    S.pack.push_back({c.src_off, S.send_n, c.count});
+                    S.send_n += c.count;
+                }
+            S.send_cnt[d] = S.send_n - S.send_off[d];
+        }
+    }
+    for (int d = 0; d < G; ++d) {
+        HaloRank &D = hr[d];
+        D.recv_halo.assign(G, -1);
+        D.recv_stage.assign(G, 0);
+        for (int s = 0; s < G; ++s) {
+            long first = -1, next = -1, n = 0;
+            bool contiguous = true;
+            for (const mpfft_copy &c : plan)
+                if (c.src == s && c.dst == d) {
+                    if (first < 0) first = c.dst_off;
+                    else if (c.dst_off != next) contiguous = false;
+                    next = c.dst_off + c.count;
+                    n += c.count;
+                }
+            if (!n) continue;
+            if (contiguous) {
+                D.recv_halo[s] = first;
+                continue;
+            }
+            D.recv_stage[s] = D.stage_n;
+            long o = D.stage_n;
+            for (const mpfft_copy &c : plan)
+                if (c.src == s && c.dst == d) {
+                    D.scatter.push_back({o, c.dst_off, c.count});
+                    o += c.count;
+                }
+            D.stage_n = o;
+        }
+    }
 }
 
 struct Arr {
@@ -137,33 +259,54 @@ struct Rank {
     u64 *host = nullptr;      // pinned staging of the operand slices
     size_t host_bytes = 0;
     Arr col[2], row[2], colc, rowc;
-    u64 *src[2] = {nullptr, nullptr};
-    u64 *halo = nullptr, *r = nullptr;
+    u64 *src[2] = {nullptr, nullptr};   // the host entry's operand slices (H2D)
+    u64 *halo = nullptr, *r = nullptr;  // the stripes' halo coefficients; the host entry's product stripes
+    int *sums = nullptr, *sums_all = nullptr;   // this rank's stripe summaries; every rank's
     void *tmp = nullptr;
     size_t tmp_bytes = 0;
-    int *sum = nullptr;
+    const u64 *in[2] = {nullptr, nullptr};   // this call's operand slices
+    u64 *out = nullptr;                      // this call's product stripes
+    u64 *hsend = nullptr, *hstage = nullptr;  // the halo's send block and staging (HaloRank)
+    Run *d_pack = nullptr, *d_scatter = nullptr;   // its run tables on the device
+    std::vector<long> tables_key;            // the partition whose tables are uploaded
 };
 
 struct Ctx {
     std::mutex mu;
     std::vector<int> devs;
     std::vector<Rank> ranks;
+    std::vector<long> key;           // the partition the halo transfers below belong to
+    std::vector<HaloRank> halo;
 };
+
+std::vector<long> part_key(const Part &p)
+{
+    return {p.n1, p.n2, (long)p.depth, (long)p.w, p.world, p.rep ? 1 : 0};
+}
 Ctx g_ctx;
 
 #define MCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { mpfft_note_hip_error(e_); return MPFFT_EHIP; } } while (0)
 
 size_t al(size_t x) { return (x + 255) / 256 * 256; }
 
+// wait for every stream of every rank: no copy engine may still read or write a buffer
+// that is about to be freed (another rank's exchange stream may be pulling from it)
+void drain(std::vector<Rank> &rk)
+{
+    for (Rank &R : rk) {
+        if (!R.s && !R.xs) continue;
+        (void)hipSetDevice(R.dev);
+        if (R.s) (void)hipStreamSynchronize(R.s);
+        if (R.xs) (void)hipStreamSynchronize(R.xs);
+    }
+}
+
+// after drain(rk)
 void free_rank(Rank &R)
 {
-    if (R.s) {
-        (void)hipSetDevice(R.dev);
-        (void)hipStreamSynchronize(R.s);
-    }
+    if (R.s || R.mem || R.host) (void)hipSetDevice(R.dev);
     if (R.mem) (void)hipFree(R.mem);
     if (R.host) (void)hipHostFree(R.host);
-    if (R.xs) (void)hipStreamSynchronize(R.xs);
     if (R.ev) (void)hipEventDestroy(R.ev);
     if (R.eva) (void)hipEventDestroy(R.eva);
     if (R.evx) (void)hipEventDestroy(R.evx);
@@ -172,8 +315,9 @@ void free_rank(Rank &R)
     R = Rank();
 }
 
-// carve rank d's arrays out of one grow-only allocation
-int setup_rank(const Part &p, int d, Rank &R)
+// carve rank d's arrays out of one grow-only allocation (host: also the operand slices, their
+// pinned staging and the product stripes)
+int setup_rank(const Part &p, int d, Rank &R, bool host, const HaloRank &HR)
 {
     MCHK(hipSetDevice(R.dev));
     if (!R.s) MCHK(hipStreamCreateWithFlags(&R.s, hipStreamNonBlocking));
@@ -182,21 +326,29 @@ int setup_rank(const Part &p, int d, Rank &R)
     if (!R.eva) MCHK(hipEventCreateWithFlags(&R.eva, hipEventDisableTiming));
     if (!R.evx) MCHK(hipEventCreateWithFlags(&R.evx, hipEventDisableTiming));
     const long cs = p.NR * p.C, rs = p.rcount(d) * p.NC;
-    const long mcount = p.M[d + 1] - p.M[d];
     const bool w1 = p.world == 1;
     const int ncol = (w1 && p.fused) ? 3 : 2;          // world 1: the fused product's column array
     const int nrow = w1 ? 0 : (p.fused ? 3 : 2);      // world 1: row arrays are views
     auto arr_bytes = [&](long slots) { return al(slots * p.l * 8) + al(slots * p.cbw * 8) + al(slots * 4); };
-    const size_t tmpb = mpfft_shard_combine_tmp_bytes(mcount > 0 ? mcount : 1);
-    const long sl = p.nsl() * p.Tr * p.chunk;        // operand slices held (all blocks' when replicated)
-    const size_t need = ncol * arr_bytes(cs) + nrow * arr_bytes(rs) + 2 * al(sl * 8) +
-                        al(p.H * p.l * 8) + al((mcount > 0 ? mcount : 1) * 8) + al(tmpb) + 256;
+    const size_t ctb = mpfft_shard_combine_tmp_bytes(p.n1, p.n2, p.depth, p.w, p.world);
+    const long sl = p.src_limbs();                    // operand slices held (all blocks' when replicated)
+    const size_t need = ncol * arr_bytes(cs) + nrow * arr_bytes(rs) + (host ? 2 * al(sl * 8) + al(p.Tr * p.SL * 8) : 0) +
+                        al(p.Tr * p.H * p.l * 8) + al(p.Tr * 2 * 4) + al(p.world * p.Tr * 2 * 4) + al(ctb) +
+                        al(HR.send_n * 8) + al(HR.stage_n * 8) + al(HR.pack.size() * sizeof(Run)) +
+                        al(HR.scatter.size() * sizeof(Run)) + 256;
     if (R.mem_bytes < need) {
-        if (R.mem) MCHK(hipFree(R.mem));
+        if (R.mem) {
+            (void)hipStreamSynchronize(R.s);
+            MCHK(hipFree(R.mem));
+        }
         R.mem = nullptr;
         R.mem_bytes = 0;
-        if (hipMalloc((void **)&R.mem, need) != hipSuccess) return MPFFT_ENOMEM;
+        if (hipMalloc((void **)&R.mem, need) != hipSuccess) {
+            (void)hipGetLastError();
+            return MPFFT_ENOMEM;
+        }
         R.mem_bytes = need;
+        R.tables_key.clear();
         MCHK(hipMemsetAsync(R.mem, 0, need, R.s));   // zero carry masks / carry limbs, as sharded.py
     }
     unsigned char *q = R.mem;
@@ -219,20 +371,43 @@ int setup_rank(const Part &p, int d, Rank &R)
         R.row[1] = carve(rs);
         R.rowc = p.fused ? carve(rs) : Arr();
     }
-    R.src[0] = (u64 *)q; q += al(sl * 8);
-    R.src[1] = (u64 *)q; q += al(sl * 8);
-    R.halo = (u64 *)q; q += al(p.H * p.l * 8);
-    R.r = (u64 *)q; q += al((mcount > 0 ? mcount : 1) * 8);
-    R.tmp = q; q += al(tmpb);
-    R.tmp_bytes = tmpb;
-    R.sum = (int *)q;
-    const size_t hb = (size_t)2 * sl * 8;
-    if (R.host_bytes < hb) {
-        if (R.host) MCHK(hipHostFree(R.host));
-        R.host = nullptr;
-        R.host_bytes = 0;
-        if (hipHostMalloc((void **)&R.host, hb, hipHostMallocDefault) != hipSuccess) return MPFFT_ENOMEM;
-        R.host_bytes = hb;
+    R.halo = (u64 *)q; q += al(p.Tr * p.H * p.l * 8);
+    R.sums = (int *)q; q += al(p.Tr * 2 * 4);
+    R.sums_all = (int *)q; q += al(p.world * p.Tr * 2 * 4);
+    R.tmp = q; q += al(ctb);
+    R.tmp_bytes = ctb;
+    R.hsend = (u64 *)q; q += al(HR.send_n * 8);
+    R.hstage = (u64 *)q; q += al(HR.stage_n * 8);
+    R.d_pack = (Run *)q; q += al(HR.pack.size() * sizeof(Run));
+    R.d_scatter = (Run *)q; q += al(HR.scatter.size() * sizeof(Run));
+    const std::vector<long> key = part_key(p);
+    if (R.tables_key != key) {   // the run tables: once per partition (the carve is deterministic)
+        if (!HR.pack.empty())
+            MCHK(hipMemcpyAsync(R.d_pack, HR.pack.data(), HR.pack.size() * sizeof(Run), hipMemcpyHostToDevice, R.s));
+        if (!HR.scatter.empty())
+            MCHK(hipMemcpyAsync(R.d_scatter, HR.scatter.data(), HR.scatter.size() * sizeof(Run),
+                                hipMemcpyHostToDevice, R.s));
+        MCHK(hipStreamSynchronize(R.s));   // (pageable sources)
+        R.tables_key = key;
+    }
+    if (host) {
+        R.src[0] = (u64 *)q; q += al(sl * 8);
+        R.src[1] = (u64 *)q; q += al(sl * 8);
+        R.r = (u64 *)q; q += al(p.Tr * p.SL * 8);
+        const size_t hb = (size_t)2 * sl * 8;
+        if (R.host_bytes < hb) {
+            if (R.host) MCHK(hipHostFree(R.host));
+            R.host = nullptr;
+            R.host_bytes = 0;
+            if (hipHostMalloc((void **)&R.host, hb, hipHostMallocDefault) != hipSuccess) {
+                (void)hipGetLastError();
+                return MPFFT_ENOMEM;
+            }
+            R.host_bytes = hb;
+        }
+    } else {
+        R.src[0] = R.src[1] = nullptr;
+        R.r = nullptr;
     }
     return MPFFT_OK;
 }
@@ -268,18 +443,22 @@ mpfft_shard desc(const Part &p, int d, const Rank &R, unsigned long depth, unsig
 }
 
 // rank d's column slices of operand a: for each live row position q, `chunk` limbs from limb
-// floor((q NC + d C) bits1 / 64) on (ShardPlan.slice_operand)
-void pack_slice(const Part &p, int d, const u64 *a, long na, u64 *out)
+// floor((q NC + blk C) bits1 / 64) on (ShardPlan.slice_operand), for its own column block, or
+// for every block in turn when the forward columns are replicated
+void pack_slices(const Part &p, int d, const u64 *a, long na, u64 *out)
 {
-    for (long q = 0; q < p.Tr; ++q) {
-        u64 *o = out + q * p.chunk;
-        const long s0 = (long)(((unsigned __int128)(q * p.NC + d * p.C) * (u64)p.bits1) / 64);
-        long cnt = 0;
-        if (s0 < na) {
-            cnt = na - s0 < p.chunk ? na - s0 : p.chunk;
-            memcpy(o, a + s0, (size_t)cnt * 8);
+    for (long e = 0; e < p.nsl(); ++e) {
+        const long blk = p.rep ? e : d;
+        for (long q = 0; q < p.Tr; ++q) {
+            u64 *o = out + (e * p.Tr + q) * p.chunk;
+            const long s0 = (long)(((unsigned __int128)(q * p.NC + blk * p.C) * (u64)p.bits1) / 64);
+            long cnt = 0;
+            if (s0 < na) {
+                cnt = na - s0 < p.chunk ? na - s0 : p.chunk;
+                memcpy(o, a + s0, (size_t)cnt * 8);
+            }
+            if (cnt < p.chunk) memset(o + cnt, 0, (size_t)(p.chunk - cnt) * 8);
         }
-        if (cnt < p.chunk) memset(o + cnt, 0, (size_t)(p.chunk - cnt) * 8);
     }
 }
 
@@ -290,26 +469,24 @@ void *field_ptr(const Arr &a, int f, long off)
     return a.top + off;
 }
 
-// queue one copy of an exchange plan on stream `st` of its receiving rank
+void *loc(const Rank &R, int layout, int op, int field, long off)
+{
+    if (layout == MPFFT_LAYOUT_HALO) return R.halo + off;
+    return field_ptr(layout ? R.row[op] : R.col[op], field, off);
+}
+
+// queue one copy of an exchange or halo plan on stream `st` of its receiving rank
 int queue_copy(const std::vector<Rank> &rk, const mpfft_copy &c, hipStream_t st)
 {
     const Rank &S = rk[c.src], &D = rk[c.dst];
-    const Arr &sa = c.src_layout ? S.row[c.op] : S.col[c.op];
-    const Arr &da = c.dst_layout ? D.row[c.op] : D.col[c.op];
     const size_t es = c.field == 2 ? 4 : 8;
-    void *dp = field_ptr(da, c.field, c.dst_off);
-    const void *sp = field_ptr(sa, c.field, c.src_off);
+    void *dp = loc(D, c.dst_layout, c.op, c.field, c.dst_off);
+    const void *sp = loc(S, c.src_layout, c.op, c.field, c.src_off);
     if (dp == sp) return MPFFT_OK;   // world 1: the row layout is a view of the column layout
     if (S.dev == D.dev) MCHK(hipMemcpyAsync(dp, sp, c.count * es, hipMemcpyDeviceToDevice, st));
     else MCHK(hipMemcpyPeerAsync(dp, D.dev, sp, S.dev, c.count * es, st));
     return MPFFT_OK;
 }
-
-// exchange #1 with the forward column passes run per operand: every receiver's exchange
-// stream pulls operand 1's blocks once all senders finished operand 1's passes (event eva)
-// -- while the compute streams run operand 2's passes -- then operand 2's (event ev); the
-// compute stream waits for both before the row passes
-int run_exchange_fwd(const Part &p, std::vector<Rank> &rk);
 
 // replicated forward columns (world 2): rank d runs every column block e's split + column
 // passes from block e's operand slices into its own column arrays (scratch), then plays
@@ -325,7 +502,7 @@ int fwd_replicated(const Part &p, std::vector<Rank> &rk, unsigned long depth, un
         for (int e = 0; e < p.world; ++e) {
             mpfft_shard sh = desc(p, d, R, depth, w);
             sh.c0 = (int)(e * p.C);
-            int rc = mpfft_shard_stage(MPFFT_SHARD_FWD_COLUMNS, &sh, R.src[0] + e * sl, R.src[1] + e * sl, R.s);
+            int rc = mpfft_shard_stage(MPFFT_SHARD_FWD_COLUMNS, &sh, R.in[0] + e * sl, R.in[1] + e * sl, R.s);
             if (rc) return rc;
             for (const mpfft_copy &c : plan)
                 if (c.dst == d && c.src == e) {
@@ -339,6 +516,10 @@ int fwd_replicated(const Part &p, std::vector<Rank> &rk, unsigned long depth, un
     return MPFFT_OK;
 }
 
+// exchange #1 with the forward column passes run per operand: every receiver's exchange
+// stream pulls operand 1's blocks once all senders finished operand 1's passes (event eva)
+// -- while the compute streams run operand 2's passes -- then operand 2's (event ev); the
+// compute stream waits for both before the row passes
 int run_exchange_fwd(const Part &p, std::vector<Rank> &rk)
 {
     std::vector<mpfft_copy> plan;
@@ -364,11 +545,10 @@ int run_exchange_fwd(const Part &p, std::vector<Rank> &rk)
     return MPFFT_OK;
 }
 
-// queue one exchange: each receiver waits for every sender's last event, then pulls
-int run_exchange(const Part &p, std::vector<Rank> &rk, int which)
+// queue a set of copies (an exchange or the halo): each receiver waits for every sender's last
+// event, then pulls
+int run_copies(const Part &p, std::vector<Rank> &rk, const std::vector<mpfft_copy> &plan)
 {
-    std::vector<mpfft_copy> plan;
-    exchange_plan(p, which, plan);
     for (int d = 0; d < p.world; ++d) {
         MCHK(hipSetDevice(rk[d].dev));
         for (int s = 0; s < p.world; ++s)
@@ -393,13 +573,102 @@ int stage_all(const Part &p, std::vector<Rank> &rk, int stage, unsigned long dep
         Rank &R = rk[d];
         MCHK(hipSetDevice(R.dev));
         const mpfft_shard sh = desc(p, d, R, depth, w);
-        int rc = mpfft_shard_stage(stage, &sh, R.src[0], R.src[1], R.s);
+        int rc = mpfft_shard_stage(stage, &sh, R.in[0], R.in[1], R.s);
         if (rc) return rc;
         if (stage == MPFFT_SHARD_POINTWISE && p.fused) {   // the product is in rowc: operand 0 from here on
             std::swap(R.row[0], R.rowc);
             if (p.world == 1) std::swap(R.col[0], R.colc);
         }
         MCHK(hipEventRecord(ev_a ? R.eva : R.ev, R.s));
+    }
+    return MPFFT_OK;
+}
+
+// the halo: every sender packs its outgoing runs (one launch), every receiver pulls one block
+// per sender after that sender's pack, and scatters the blocks that are not contiguous in its halo
+int run_halo(const Part &p, std::vector<Rank> &rk, const std::vector<HaloRank> &hr)
+{
+    for (int s = 0; s < p.world; ++s) {
+        Rank &S = rk[s];
+        MCHK(hipSetDevice(S.dev));
+        if (!hr[s].pack.empty()) {
+            hipLaunchKernelGGL(k_copy_runs, dim3((unsigned)std::min<size_t>(hr[s].pack.size(), 4096)), dim3(256), 0, S.s,
+                               (const Run *)S.d_pack, (long)hr[s].pack.size(), (const u64 *)S.col[0].dig, S.hsend);
+            MCHK(hipGetLastError());
+        }
+        MCHK(hipEventRecord(S.ev, S.s));
+    }
+    for (int d = 0; d < p.world; ++d) {
+        Rank &D = rk[d];
+        MCHK(hipSetDevice(D.dev));
+        for (int s = 0; s < p.world; ++s) {
+            const Rank &S = rk[s];
+            const long n = hr[s].send_cnt[d];
+            if (!n) continue;
+            if (s != d) MCHK(hipStreamWaitEvent(D.s, S.ev, 0));
+            u64 *dp = hr[d].recv_halo[s] >= 0 ? D.halo + hr[d].recv_halo[s] : D.hstage + hr[d].recv_stage[s];
+            const u64 *sp = S.hsend + hr[s].send_off[d];
+            if (S.dev == D.dev) MCHK(hipMemcpyAsync(dp, sp, (size_t)n * 8, hipMemcpyDeviceToDevice, D.s));
+            else MCHK(hipMemcpyPeerAsync(dp, D.dev, sp, S.dev, (size_t)n * 8, D.s));
+        }
+        if (!hr[d].scatter.empty()) {
+            hipLaunchKernelGGL(k_copy_runs, dim3((unsigned)std::min<size_t>(hr[d].scatter.size(), 4096)), dim3(256), 0,
+                               D.s, (const Run *)D.d_scatter, (long)hr[d].scatter.size(), (const u64 *)D.hstage, D.halo);
+            MCHK(hipGetLastError());
+        }
+    }
+    for (int d = 0; d < p.world; ++d) {
+        MCHK(hipSetDevice(rk[d].dev));
+        MCHK(hipEventRecord(rk[d].ev, rk[d].s));
+    }
+    return MPFFT_OK;
+}
+
+// the whole multiply from every rank's operand slices (R.in) to its product stripes (R.out),
+// queued on the ranks' streams with no host synchronisation
+int run_ranks(const Part &p, std::vector<Rank> &rk, const std::vector<HaloRank> &halo, unsigned long depth,
+              unsigned long w)
+{
+    int rc;
+    if (p.rep) {
+        if ((rc = fwd_replicated(p, rk, depth, w))) return rc;
+    } else {
+        if ((rc = stage_all(p, rk, MPFFT_SHARD_FWD_COLUMNS_A, depth, w, true))) return rc;
+        if ((rc = stage_all(p, rk, MPFFT_SHARD_FWD_COLUMNS_B, depth, w))) return rc;
+        if ((rc = run_exchange_fwd(p, rk))) return rc;
+    }
+    if ((rc = stage_all(p, rk, MPFFT_SHARD_FWD_ROWS, depth, w))) return rc;
+    if ((rc = stage_all(p, rk, MPFFT_SHARD_POINTWISE, depth, w))) return rc;
+    if ((rc = stage_all(p, rk, MPFFT_SHARD_INV_ROWS, depth, w))) return rc;
+    std::vector<mpfft_copy> plan;
+    exchange_plan(p, MPFFT_XCHG_ROW_TO_COL, plan);
+    if ((rc = run_copies(p, rk, plan))) return rc;
+    if ((rc = stage_all(p, rk, MPFFT_SHARD_INV_COLUMNS, depth, w))) return rc;
+    if ((rc = run_halo(p, rk, halo))) return rc;
+    // combine phase 0: every stripe with carry-in 0 and its (generate, propagate) summary
+    for (int d = 0; d < p.world; ++d) {
+        Rank &R = rk[d];
+        MCHK(hipSetDevice(R.dev));
+        const mpfft_shard sh = desc(p, d, R, depth, w);
+        if ((rc = mpfft_shard_combine(&sh, 0, R.out, R.halo, R.sums, nullptr, R.tmp, R.tmp_bytes, R.s))) return rc;
+        MCHK(hipEventRecord(R.ev, R.s));
+    }
+    // every rank's summaries to every rank (Tr pairs each), then phase 1: each rank scans the
+    // stripes below each of its own on the device and adds the carry
+    const size_t sb = (size_t)p.Tr * 2 * sizeof(int);
+    for (int d = 0; d < p.world; ++d) {
+        Rank &R = rk[d];
+        MCHK(hipSetDevice(R.dev));
+        for (int e = 0; e < p.world; ++e) {
+            const Rank &E = rk[e];
+            if (e != d) MCHK(hipStreamWaitEvent(R.s, E.ev, 0));
+            int *dp = R.sums_all + (size_t)e * p.Tr * 2;
+            if (E.dev == R.dev) MCHK(hipMemcpyAsync(dp, E.sums, sb, hipMemcpyDeviceToDevice, R.s));
+            else MCHK(hipMemcpyPeerAsync(dp, R.dev, E.sums, E.dev, sb, R.s));
+        }
+        const mpfft_shard sh = desc(p, d, R, depth, w);
+        if ((rc = mpfft_shard_combine(&sh, 1, R.out, R.halo, R.sums, R.sums_all, R.tmp, R.tmp_bytes, R.s))) return rc;
+        MCHK(hipEventRecord(R.ev, R.s));
     }
     return MPFFT_OK;
 }
@@ -417,6 +686,33 @@ void enable_peers(const std::vector<int> &devs)
         }
 }
 
+// the context for this device list (buffers set up for partition p)
+int prepare(Ctx &X, const Part &p, const std::vector<int> &devs, bool host)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return MPFFT_ENODEV;
+    for (int d : devs)
+        if (d < 0 || d >= ndev) return MPFFT_ENODEV;
+    if (X.devs != devs) {
+        drain(X.ranks);
+        for (Rank &R : X.ranks) free_rank(R);
+        X.ranks.assign(devs.size(), Rank());
+        for (size_t g = 0; g < devs.size(); ++g) X.ranks[g].dev = devs[g];
+        X.devs = devs;
+        enable_peers(devs);
+    }
+    const std::vector<long> key = part_key(p);
+    if (X.key != key) {
+        halo_xfer(p, X.halo);
+        X.key = key;
+    }
+    for (int d = 0; d < p.world; ++d) {
+        int rc = setup_rank(p, d, X.ranks[d], host, X.halo[d]);
+        if (rc) return rc;
+    }
+    return MPFFT_OK;
+}
+
 int mul_multi_locked(Ctx &X, uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i2, long n2,
                      unsigned long depth, unsigned long w, const std::vector<int> &devs)
 {
@@ -424,27 +720,8 @@ int mul_multi_locked(Ctx &X, uint64_t *r1, const uint64_t *i1, long n1, const ui
     const int G = (int)devs.size();
     int rc = partition(p, n1, n2, depth, w, G);
     if (rc) return rc;
-    // replicated forward columns at two ranks (sharded.py ShardedMul.replicates: exchange #1
-    // there is one xGMI link carrying the other rank's rows of both column blocks; the second column block
-    // is one more column phase of HBM-bound passes); MPFFT_REPLICATE_COLUMNS=0/1 overrides
-    {
-        const char *e = getenv("MPFFT_REPLICATE_COLUMNS");
-        p.rep = e ? (e[0] == '1' && G > 1) : G == 2;
-    }
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return MPFFT_ENODEV;
-    for (int d : devs)
-        if (d < 0 || d >= ndev) return MPFFT_ENODEV;
-    if (X.devs != devs) {
-        for (Rank &R : X.ranks) free_rank(R);
-        X.ranks.assign(G, Rank());
-        for (int g = 0; g < G; ++g) X.ranks[g].dev = devs[g];
-        X.devs = devs;
-        enable_peers(devs);
-    }
+    if ((rc = prepare(X, p, devs, true))) return rc;
     std::vector<Rank> &rk = X.ranks;
-    for (int d = 0; d < G; ++d)
-        if ((rc = setup_rank(p, d, rk[d]))) return rc;
 
     // operand slices: packed and copied by one host thread per rank
     std::vector<int> trc(G, MPFFT_OK);
@@ -453,98 +730,79 @@ int mul_multi_locked(Ctx &X, uint64_t *r1, const uint64_t *i1, long n1, const ui
         for (int d = 0; d < G; ++d)
             th.emplace_back([&, d] {
                 Rank &R = rk[d];
-                const long sl = p.Tr * p.chunk, ns = p.nsl();
-                u64 *h0 = R.host, *h1 = R.host + ns * sl;
-                for (long e = 0; e < ns; ++e) {   // replicated: every block's slices, block e at e sl
-                    const int blk = p.rep ? (int)e : d;
-                    pack_slice(p, blk, i1, n1, h0 + e * sl);
-                    pack_slice(p, blk, i2, n2, h1 + e * sl);
-                }
+                const long sl = p.src_limbs();
+                pack_slices(p, d, i1, n1, R.host);
+                pack_slices(p, d, i2, n2, R.host + sl);
                 if (hipSetDevice(R.dev) != hipSuccess ||
-                    hipMemcpyAsync(R.src[0], h0, (size_t)ns * sl * 8, hipMemcpyHostToDevice, R.s) != hipSuccess ||
-                    hipMemcpyAsync(R.src[1], h1, (size_t)ns * sl * 8, hipMemcpyHostToDevice, R.s) != hipSuccess)
+                    hipMemcpyAsync(R.src[0], R.host, (size_t)sl * 8, hipMemcpyHostToDevice, R.s) != hipSuccess ||
+                    hipMemcpyAsync(R.src[1], R.host + sl, (size_t)sl * 8, hipMemcpyHostToDevice, R.s) != hipSuccess)
                     trc[d] = MPFFT_EHIP;
             });
         for (auto &t : th) t.join();
         for (int d = 0; d < G; ++d)
             if (trc[d]) return trc[d];
     }
-
-    if (p.rep) {
-        if ((rc = fwd_replicated(p, rk, depth, w))) return rc;
-    } else {
-        if ((rc = stage_all(p, rk, MPFFT_SHARD_FWD_COLUMNS_A, depth, w, true))) return rc;
-        if ((rc = stage_all(p, rk, MPFFT_SHARD_FWD_COLUMNS_B, depth, w))) return rc;
-        if ((rc = run_exchange_fwd(p, rk))) return rc;
-    }
-    if ((rc = stage_all(p, rk, MPFFT_SHARD_FWD_ROWS, depth, w))) return rc;
-    if ((rc = stage_all(p, rk, MPFFT_SHARD_POINTWISE, depth, w))) return rc;
-    if ((rc = stage_all(p, rk, MPFFT_SHARD_INV_ROWS, depth, w))) return rc;
-    if ((rc = run_exchange(p, rk, MPFFT_XCHG_ROW_TO_COL))) return rc;
-    if ((rc = stage_all(p, rk, MPFFT_SHARD_INV_COLUMNS, depth, w))) return rc;
-    if ((rc = run_exchange(p, rk, MPFFT_XCHG_COEFFS))) return rc;
-
-    // halo: the last H coefficients of rank d-1's range (its row layout) -> rank d
-    for (int d = 1; d < G; ++d) {
-        Rank &R = rk[d], &S = rk[d - 1];
-        MCHK(hipSetDevice(R.dev));
-        MCHK(hipStreamWaitEvent(R.s, S.ev, 0));
-        const long r0 = p.rows[d - 1], rc_ = p.rcount(d - 1), kend = p.rows[d] * p.NC;
-        for (long h = 0; h < p.H; ++h) {
-            const long k = kend - p.H + h, pp = k / p.NC - r0, cc = k % p.NC;
-            const long slot = (cc / p.C) * (rc_ * p.C) + pp * p.C + (cc % p.C);
-            const u64 *sp = S.row[0].dig + slot * p.l;
-            u64 *dp = R.halo + h * p.l;
-            if (S.dev == R.dev) MCHK(hipMemcpyAsync(dp, sp, (size_t)p.l * 8, hipMemcpyDeviceToDevice, R.s));
-            else MCHK(hipMemcpyPeerAsync(dp, R.dev, sp, S.dev, (size_t)p.l * 8, R.s));
-        }
-    }
-
-    // combine phase 0, the cross-rank carry (generate, propagate per rank), phase 1
-    std::vector<int> sums(2 * G, 0);
     for (int d = 0; d < G; ++d) {
-        Rank &R = rk[d];
-        MCHK(hipSetDevice(R.dev));
-        const mpfft_shard sh = desc(p, d, R, depth, w);
-        const long mcount = p.M[d + 1] - p.M[d];
-        if (mcount < 1) continue;
-        rc = mpfft_shard_combine(&sh, 0, R.r, p.M[d], mcount, p.rows[d] * p.NC, d ? R.halo : nullptr,
-                                 d ? (int)p.H : 0, R.tmp, R.tmp_bytes, 0, R.sum, R.s);
-        if (rc) return rc;
-        MCHK(hipMemcpyAsync(&sums[2 * d], R.sum, 2 * sizeof(int), hipMemcpyDeviceToHost, R.s));
+        rk[d].in[0] = rk[d].src[0];
+        rk[d].in[1] = rk[d].src[1];
+        rk[d].out = rk[d].r;
     }
-    for (int d = 0; d < G; ++d) {
-        MCHK(hipSetDevice(rk[d].dev));
-        MCHK(hipStreamSynchronize(rk[d].s));
-    }
-    int cin = 0;
-    for (int d = 0; d < G; ++d) {
-        Rank &R = rk[d];
-        const long mcount = p.M[d + 1] - p.M[d];
-        if (mcount >= 1 && cin) {
-            MCHK(hipSetDevice(R.dev));
-            const mpfft_shard sh = desc(p, d, R, depth, w);
-            rc = mpfft_shard_combine(&sh, 1, R.r, p.M[d], mcount, p.rows[d] * p.NC, d ? R.halo : nullptr,
-                                     d ? (int)p.H : 0, R.tmp, R.tmp_bytes, 1, R.sum, R.s);
-            if (rc) return rc;
-        }
-        if (mcount >= 1) cin = (sums[2 * d] || (sums[2 * d + 1] && cin)) ? 1 : 0;
-    }
-    // product limbs: one thread per rank (pageable destination)
+    if ((rc = run_ranks(p, rk, X.halo, depth, w))) return rc;
+    // product stripes into their places in r1: one thread per rank (pageable destination)
     {
         std::vector<std::thread> th;
         for (int d = 0; d < G; ++d)
             th.emplace_back([&, d] {
                 Rank &R = rk[d];
-                const long mcount = p.M[d + 1] - p.M[d];
                 if (hipSetDevice(R.dev) != hipSuccess) { trc[d] = MPFFT_EHIP; return; }
-                if (mcount > 0 && hipMemcpyAsync(r1 + p.M[d], R.r, (size_t)mcount * 8, hipMemcpyDeviceToHost, R.s) != hipSuccess)
-                    trc[d] = MPFFT_EHIP;
+                for (long j = 0; j < p.Tr && !trc[d]; ++j) {
+                    const long s = j * G + d, cnt = p.ms[s + 1] - p.ms[s];
+                    if (cnt > 0 && hipMemcpyAsync(r1 + p.ms[s], R.r + j * p.SL, (size_t)cnt * 8, hipMemcpyDeviceToHost,
+                                                  R.s) != hipSuccess)
+                        trc[d] = MPFFT_EHIP;
+                }
                 if (hipStreamSynchronize(R.s) != hipSuccess) trc[d] = MPFFT_EHIP;
             });
         for (auto &t : th) t.join();
         for (int d = 0; d < G; ++d)
             if (trc[d]) return trc[d];
+    }
+    return MPFFT_OK;
+}
+
+int mul_multi_device_locked(Ctx &X, long n1, long n2, unsigned long depth, unsigned long w,
+                            const std::vector<int> &devs, const uint64_t *const *d_src1,
+                            const uint64_t *const *d_src2, uint64_t *const *d_r, void *const *streams)
+{
+    Part p;
+    const int G = (int)devs.size();
+    int rc = partition(p, n1, n2, depth, w, G);
+    if (rc) return rc;
+    if (!d_src1 || !d_src2 || !d_r) return MPFFT_EINVAL;
+    if ((rc = prepare(X, p, devs, false))) return rc;
+    std::vector<Rank> &rk = X.ranks;
+    for (int d = 0; d < G; ++d) {
+        Rank &R = rk[d];
+        if (!d_src1[d] || !d_src2[d] || !d_r[d]) return MPFFT_EINVAL;
+        R.in[0] = d_src1[d];
+        R.in[1] = d_src2[d];
+        R.out = d_r[d];
+        if (streams && streams[d]) {   // after the caller's work on its stream
+            MCHK(hipSetDevice(R.dev));
+            MCHK(hipEventRecord(R.ev, (hipStream_t)streams[d]));
+            MCHK(hipStreamWaitEvent(R.s, R.ev, 0));
+        }
+    }
+    if ((rc = run_ranks(p, rk, X.halo, depth, w))) return rc;
+    for (int d = 0; d < G; ++d) {
+        Rank &R = rk[d];
+        MCHK(hipSetDevice(R.dev));
+        if (streams && streams[d]) {   // the caller's stream continues after the product
+            MCHK(hipEventRecord(R.ev, R.s));
+            MCHK(hipStreamWaitEvent((hipStream_t)streams[d], R.ev, 0));
+        } else {
+            MCHK(hipStreamSynchronize(R.s));
+        }
     }
     return MPFFT_OK;
 }
@@ -556,6 +814,20 @@ struct Policy {
     long min_l = 1024;
 };
 Policy g_pol;
+
+// a device list every id of which exists (else the policy stays off: products run on the
+// calling thread's device)
+bool devices_exist(const std::vector<int> &v)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    for (int d : v)
+        if (d < 0 || d >= ndev) return false;
+    return true;
+}
 
 void policy_init_locked()
 {
@@ -573,7 +845,7 @@ void policy_init_locked()
         q = *end == ',' ? end + 1 : end;
         if (*end != ',') break;
     }
-    if (v.size() > 1) g_pol.devs = v;
+    if (v.size() > 1 && devices_exist(v)) g_pol.devs = v;
 }
 
 }  // namespace
@@ -581,36 +853,67 @@ void policy_init_locked()
 // used by mpfft_mul_ex (mpfft.hip): the device list the policy picks for this product, if any
 int mpfft_multi_policy(long n1, long n2, unsigned long depth, unsigned long w, std::vector<int> &devs)
 {
+    long min_l;
     {
         std::lock_guard<std::mutex> lk(g_pol.mu);
         policy_init_locked();
         if (g_pol.devs.size() < 2) return 0;
         devs = g_pol.devs;
+        min_l = g_pol.min_l;
     }
     long info[10];
-    if (mpfft_plan_info(n1, n2, depth, w, info) || info[1] < g_pol.min_l) return 0;
+    if (mpfft_plan_info(n1, n2, depth, w, info) || info[1] < min_l) return 0;
     Part p;
     return partition(p, n1, n2, depth, w, (int)devs.size()) == MPFFT_OK ? (int)devs.size() : 0;
 }
 
+namespace {
+// leave no work queued behind a failed call: compute and exchange streams of every rank
+int finish(Ctx &X, int rc, int cur)
+{
+    if (rc) drain(X.ranks);
+    (void)hipSetDevice(cur);
+    return rc;
+}
+}  // namespace
+
 extern "C" {
 
-int mpfft_shard_partition(long n1, long n2, unsigned long depth, unsigned long w, int world, long *rows, long *M,
-                          long *info)
+int mpfft_shard_partition(long n1, long n2, unsigned long depth, unsigned long w, int world, long *rows, long *info)
 {
     Part p;
     int rc = partition(p, n1, n2, depth, w, world);
     if (rc) return rc;
-    for (int d = 0; d <= world; ++d) {
-        rows[d] = p.rows[d];
-        M[d] = p.M[d];
-    }
+    for (int d = 0; d <= world; ++d) rows[d] = p.rows[d];
     info[0] = p.C;
     info[1] = p.chunk;
     info[2] = p.H;
     info[3] = p.Tr;
     info[4] = p.fused ? 1 : 0;
+    info[5] = p.SL;
+    info[6] = p.S;
     return MPFFT_OK;
+}
+
+long mpfft_shard_stripes(long n1, long n2, unsigned long depth, unsigned long w, int world, long *ms, long cap)
+{
+    Part p;
+    int rc = partition(p, n1, n2, depth, w, world);
+    if (rc) return -rc;
+    if (ms) {
+        if (cap < p.S + 1) return -MPFFT_EINVAL;
+        memcpy(ms, p.ms.data(), (size_t)(p.S + 1) * sizeof(long));
+    }
+    return p.S + 1;
+}
+
+static long copy_out(const std::vector<mpfft_copy> &v, mpfft_copy *out, long cap)
+{
+    if (out) {
+        if (cap < (long)v.size()) return -MPFFT_EINVAL;
+        memcpy(out, v.data(), v.size() * sizeof(mpfft_copy));
+    }
+    return (long)v.size();
 }
 
 long mpfft_shard_exchange_plan(long n1, long n2, unsigned long depth, unsigned long w, int world, int which,
@@ -619,14 +922,39 @@ long mpfft_shard_exchange_plan(long n1, long n2, unsigned long depth, unsigned l
     Part p;
     int rc = partition(p, n1, n2, depth, w, world);
     if (rc) return -rc;
-    if (which < MPFFT_XCHG_COL_TO_ROW || which > MPFFT_XCHG_COEFFS) return -MPFFT_EINVAL;
+    if (which != MPFFT_XCHG_COL_TO_ROW && which != MPFFT_XCHG_ROW_TO_COL) return -MPFFT_EINVAL;
     std::vector<mpfft_copy> v;
     exchange_plan(p, which, v);
-    if (out) {
-        if (cap < (long)v.size()) return -MPFFT_EINVAL;
-        memcpy(out, v.data(), v.size() * sizeof(mpfft_copy));
-    }
-    return (long)v.size();
+    return copy_out(v, out, cap);
+}
+
+long mpfft_shard_halo_plan(long n1, long n2, unsigned long depth, unsigned long w, int world, mpfft_copy *out,
+                           long cap)
+{
+    Part p;
+    int rc = partition(p, n1, n2, depth, w, world);
+    if (rc) return -rc;
+    std::vector<mpfft_copy> v;
+    halo_plan(p, v);
+    return copy_out(v, out, cap);
+}
+
+long mpfft_shard_src_limbs(long n1, long n2, unsigned long depth, unsigned long w, int world)
+{
+    Part p;
+    int rc = partition(p, n1, n2, depth, w, world);
+    return rc ? -rc : p.src_limbs();
+}
+
+int mpfft_shard_pack(long n1, long n2, unsigned long depth, unsigned long w, int world, int rank, const uint64_t *a,
+                     long na, uint64_t *out)
+{
+    Part p;
+    int rc = partition(p, n1, n2, depth, w, world);
+    if (rc) return rc;
+    if (rank < 0 || rank >= world || !a || !out || na < 0) return MPFFT_EINVAL;
+    pack_slices(p, rank, a, na, out);
+    return MPFFT_OK;
 }
 
 int mpfft_mul_multi(uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i2, long n2, unsigned long depth,
@@ -639,16 +967,21 @@ int mpfft_mul_multi(uint64_t *r1, const uint64_t *i1, long n1, const uint64_t *i
     (void)hipGetDevice(&cur);
     std::lock_guard<std::mutex> lk(g_ctx.mu);
     (void)hipGetLastError();
-    const int rc = mul_multi_locked(g_ctx, r1, i1, n1, i2, n2, depth, w, devs);
-    if (rc) {   // leave no work queued behind a failed call
-        for (Rank &R : g_ctx.ranks)
-            if (R.s) {
-                (void)hipSetDevice(R.dev);
-                (void)hipStreamSynchronize(R.s);
-            }
-    }
-    (void)hipSetDevice(cur);
-    return rc;
+    return finish(g_ctx, mul_multi_locked(g_ctx, r1, i1, n1, i2, n2, depth, w, devs), cur);
+}
+
+int mpfft_mul_multi_device(long n1, long n2, unsigned long depth, unsigned long w, int ngpus, const int *devices,
+                           const uint64_t *const *d_src1, const uint64_t *const *d_src2, uint64_t *const *d_r,
+                           void *const *streams)
+{
+    if (ngpus < 1) return MPFFT_EINVAL;
+    std::vector<int> devs(ngpus);
+    for (int g = 0; g < ngpus; ++g) devs[g] = devices ? devices[g] : g;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    std::lock_guard<std::mutex> lk(g_ctx.mu);
+    (void)hipGetLastError();
+    return finish(g_ctx, mul_multi_device_locked(g_ctx, n1, n2, depth, w, devs, d_src1, d_src2, d_r, streams), cur);
 }
 
 int mpfft_multi_release(void)
@@ -656,6 +989,7 @@ int mpfft_multi_release(void)
     std::lock_guard<std::mutex> lk(g_ctx.mu);
     int cur = 0;
     (void)hipGetDevice(&cur);
+    drain(g_ctx.ranks);
     for (Rank &R : g_ctx.ranks) free_rank(R);
     g_ctx.ranks.clear();
     g_ctx.devs.clear();
@@ -665,12 +999,13 @@ int mpfft_multi_release(void)
 
 int mpfft_set_devices(int ngpus, const int *devices, long min_l)
 {
+    std::vector<int> v;
+    if (ngpus > 1)
+        for (int g = 0; g < ngpus; ++g) v.push_back(devices ? devices[g] : g);
+    if (!v.empty() && !devices_exist(v)) return MPFFT_ENODEV;
     std::lock_guard<std::mutex> lk(g_pol.mu);
     g_pol.init = true;   // an explicit choice overrides MPFFT_DEVICES
-    g_pol.devs.clear();
-    if (ngpus > 1) {
-        for (int g = 0; g < ngpus; ++g) g_pol.devs.push_back(devices ? devices[g] : g);
-    }
+    g_pol.devs = v;
     g_pol.min_l = min_l > 0 ? min_l : 1024;
     return MPFFT_OK;
 }

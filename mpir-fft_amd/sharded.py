@@ -9,26 +9,28 @@ So:
 
   rank g owns columns [g*C, (g+1)*C), C = NC / world     (column layout)
   1. split + forward column passes of both operands on the owned columns
-  2. all-to-all #1: rows [r_d, r_{d+1}) of every column block -> rank d
+  2. exchange #1: rows [r_d, r_{d+1}) of every column block -> rank d
   3. twiddle + forward row passes, pointwise, inverse row passes on owned rows
-  4. all-to-all #2: the rows go back to their column owners
+  4. exchange #2: the rows go back to their column owners
   5. truncated inverse column transform + scaling on the owned columns
-  6. all-to-all #3: contiguous coefficient ranges -> rank d; all-gather of a
-     small halo (the few coefficients overlapping the rank's first limbs)
-  7. combine the rank's limb range; all-gather of one (generate, propagate)
-     pair per rank resolves the cross-rank carry (a scan over ranks)
+  6. halo: for each row position, the H coefficients before the rank's C columns
+  7. combine in the column layout: the rank's C columns of row position j are the C
+     consecutive coefficients [(j world + g) C, + C) -- product stripe j world + g, a
+     contiguous bit range -- combined with carry-in 0; an all-gather of every stripe's
+     (generate, propagate) pair; each stripe's carry-in added on the device
 
-The product ends up distributed: rank d holds limbs [M_d, M_{d+1}).  Exchanges
-use all_to_all_single (RCCL over xGMI on GPUs, gloo on CPU for the tests);
-no all-reduce is used.  Each exchange moves one copy of the data: #1 both
-operands, #2 and #3 one.
+The product ends up striped: rank g holds stripes j world + g (mpfft_shard_stripes gives
+their limb ranges; mpfft.assemble_stripes puts them in order).  Exchanges are batches of
+point-to-point send/recv (RCCL over xGMI on GPUs, gloo on CPU for the tests); no
+all-reduce is used.  #1 moves both operands, #2 the product once; the product never
+goes back to row owners (the reference's TODO:53-59: combine in place, for locality).
 """
 import os
 
 import numpy as np
 
 
-XCHG_COL_TO_ROW, XCHG_ROW_TO_COL, XCHG_COEFFS = 1, 2, 3   # include/mpfft.h MPFFT_XCHG_*
+XCHG_COL_TO_ROW, XCHG_ROW_TO_COL = 1, 2   # include/mpfft.h MPFFT_XCHG_*
 
 
 def cb_words(l):
@@ -59,8 +61,9 @@ class ShardPlan:
             raise ValueError(f"world={world}: too many ranks for this size ({e})") from None
         self.C = part["C"]                 # columns per rank (= column block of the row layout)
         self.rows = part["rows"]           # rank d owns live rows [rows[d], rows[d+1])
-        self.M = part["M"]                 # rank d writes product limbs [M[d], M[d+1])
-        self.H = part["H"]                 # halo: coefficients before a rank's first one that reach its limbs
+        self.H = part["H"]                 # halo: coefficients before a stripe that reach its limbs
+        self.SL, self.S = part["SL"], part["S"]   # limbs per stripe at most; stripes (world Tr)
+        self.ms = part["ms"]               # stripe s = j world + g: product limbs [ms[s], ms[s+1])
         # operand column slices (fused split reads them through SrcSlice, coeff.hpp): for
         # each live position p < Tr, `chunk` limbs from floor((p NC + c0) bits1 / 64) on
         self.chunk = part["chunk"]
@@ -72,6 +75,13 @@ class ShardPlan:
             self._xplans[which] = self.mp.shard_exchange_plan(self.n1, self.n2, self.depth, self.w, self.world,
                                                               which)
         return self._xplans[which]
+
+    def halo_plan(self):
+        """the halo copies before the combine (mpfft_shard_halo_plan): column layout -> halo,
+        offsets and counts in limbs"""
+        if "halo" not in self._xplans:
+            self._xplans["halo"] = self.mp.shard_halo_plan(self.n1, self.n2, self.depth, self.w, self.world)
+        return self._xplans["halo"]
 
     def slice_start(self, p, d):
         return ((p * self.NC + d * self.C) * self.bits1) // 64
@@ -89,6 +99,10 @@ class ShardPlan:
 
     def rcount(self, d):
         return self.rows[d + 1] - self.rows[d]
+
+    def assemble(self, stripes):
+        """the product (uint64 limbs) from every rank's stripe buffer (rank order, numpy uint64)"""
+        return self.mp.assemble_stripes({"ms": self.ms, "SL": self.SL}, self.world, stripes)
 
     def col_slots(self):
         return self.NR * self.C
@@ -196,9 +210,42 @@ class ShardedMul:
             plan.append(([v if v is not None else empty for v in send], [v if v is not None else empty for v in recv]))
         return self.comm.exchange(plan, wait=wait)
 
+    def _halo(self, halo):
+        """the H coefficients before each of this rank's stripes into `halo` (Tr H l limbs):
+        one packed message per peer, runs in the library's plan order"""
+        p, me, W = self.p, self.rank, self.p.world
+        src = self.col[0]["dig"]
+        sends, recvs = [[] for _ in range(W)], [[] for _ in range(W)]
+        for c in p.halo_plan():
+            if c["src"] == me:
+                sends[c["dst"]].append(src[c["src_off"]: c["src_off"] + c["count"]])
+            if c["dst"] == me:
+                recvs[c["src"]].append((c["dst_off"], c["count"]))
+        empty = src[:0]
+        send, recv, scatter = [], [], []
+        for d in range(W):
+            send.append(self.be.cat(sends[d]) if sends[d] else empty)
+            runs = recvs[d]
+            n = sum(cnt for _, cnt in runs)
+            if not runs:
+                recv.append(empty)
+            elif all(runs[i][0] + runs[i][1] == runs[i + 1][0] for i in range(len(runs) - 1)):
+                recv.append(halo[runs[0][0]: runs[0][0] + n])      # dst-contiguous: straight in
+            else:
+                buf = halo.new_empty(n)
+                recv.append(buf)
+                scatter.append((buf, runs))
+        self.comm.exchange([(send, recv)], wait=True)
+        for buf, runs in scatter:
+            o = 0
+            for off, cnt in runs:
+                halo[off: off + cnt].copy_(buf[o: o + cnt])
+                o += cnt
+
     def run(self, i1, i2, mark=None):
         """i1, i2: this rank's operand column slices (ShardPlan.slice_operand; the full
-        operands when sliced=False), backend arrays.  Returns (m0, limbs).
+        operands when sliced=False), backend arrays.  Returns this rank's product stripes
+        (Tr SL limbs: stripe j world + rank at j SL, ShardPlan.ms gives their limb ranges).
         mark(name), when given, is called after each phase (bench.py's per-phase events)."""
         p, be, sh = self.p, self.be, self.shard_desc()
         chunked_ok = mark is None
@@ -221,11 +268,11 @@ class ShardedMul:
             # operand 1's exchange in flight while operand 2's column passes run (on RCCL: the
             # transfers go on the communicator's stream, queued behind operand 1's passes only)
             be.stage("fwd_columns_a", sh, i1, i2)
-            pend = self._exchange(XCHG_COL_TO_ROW, op=0, wait=False)
+            pend1 = self._exchange(XCHG_COL_TO_ROW, op=0, wait=False)
             be.stage("fwd_columns_b", sh, i1, i2)
             mark("fwd_columns")
-            pend += self._exchange(XCHG_COL_TO_ROW, op=1, wait=False)
-            self.comm.wait(pend)
+            pend1 += self._exchange(XCHG_COL_TO_ROW, op=1, wait=False)
+            self.comm.wait(pend1)          # exchange #1 complete before the row passes
         else:
             be.stage("fwd_columns", sh, i1, i2)
             mark("fwd_columns")
@@ -240,15 +287,14 @@ class ShardedMul:
             if self.fused:
                 self.row[0], self.rowc = self.rowc, self.row[0]
             sh_inv = self.shard_desc()   # operand 0's row array = the product
-            pend = []
+            pend2 = []
             for i in range(R):
                 lo, hi = chunk_rows(p.rcount(self.rank), i, R)
                 be.stage_rows("fwd_rows", sh_fwd, lo, hi)
                 be.stage_rows("pointwise", sh_fwd, lo, hi)
                 be.stage_rows("inv_rows", sh_inv, lo, hi)
-                pend += self._exchange(XCHG_ROW_TO_COL, wait=False, chunk=(i, R))
+                pend2 += self._exchange(XCHG_ROW_TO_COL, wait=False, chunk=(i, R))
             mark("inv_rows")
-            self.comm.wait(pend)
             sh = sh_inv
         else:
             be.stage("fwd_rows", sh, i1, i2)
@@ -262,27 +308,21 @@ class ShardedMul:
                 sh = self.shard_desc()
             be.stage("inv_rows", sh, i1, i2)
             mark("inv_rows")
-            self._exchange(XCHG_ROW_TO_COL)
+            pend2 = self._exchange(XCHG_ROW_TO_COL, wait=False)
+        self.comm.wait(pend2)          # exchange #2 complete before the inverse columns
         mark("exchange2")
         be.stage("inv_columns", sh, i1, i2)
         mark("inv_columns")
-        self._exchange(XCHG_COEFFS)                        # canonical coefficients: limbs only
-        # halo: the last H coefficients of every rank's range, all-gathered
-        halo_all = self.comm.all_gather(be.tail_coeffs(sh, p.H))
-        mark("exchange3")
-        d = self.rank
-        m0, mcount = p.M[d], p.M[d + 1] - p.M[d]
-        kbase = p.rows[d] * p.NC
-        halo = halo_all[d - 1] if d > 0 else None
-        summary = be.combine(sh, 0, m0, mcount, kbase, halo, p.H if d else 0, cin=0)
-        sums = self.comm.all_gather(summary)               # (generate, propagate) per rank
-        cin = 0
-        for e in range(d):
-            g, pr = int(sums[e][0]), int(sums[e][1])
-            cin = 1 if (g or (pr and cin)) else 0
-        limbs = be.combine(sh, 1, m0, mcount, kbase, halo, p.H if d else 0, cin=cin)
+        # combine in the column layout: the H coefficients before each stripe, every stripe
+        # with carry-in 0, every rank's stripe summaries, each stripe's carry-in
+        halo = be.halo_buffer()
+        self._halo(halo)
+        mark("exchange_halo")
+        r, sums = be.combine(sh, 0, halo)
+        sums_all = self.comm.all_gather(sums)
+        be.combine(sh, 1, halo, sums_all)
         mark("combine")
-        return m0, limbs
+        return r
 
 
 def chunk_rows(rcount, i, R):
@@ -402,32 +442,30 @@ class GpuBackend:
                  "fwd_columns_a": 5, "fwd_columns_b": 6}[name]
         self.mp.shard_stage(which, self._desc(sh), i1, i2, self.stream)
 
-    def tail_coeffs(self, sh, H):
-        """canonical limbs of the last H coefficients of this rank's range (row layout)."""
+    def halo_buffer(self):
         p = self.p
-        r0, rc, C = sh["r0"], sh["rcount"], sh["ccb"]
-        ks = np.arange((r0 + rc) * p.NC - H, (r0 + rc) * p.NC)
-        pp, cc = ks // p.NC - r0, ks % p.NC
-        slots = (cc // C) * (rc * C) + pp * C + (cc % C)
-        dig = sh["row"][0]["dig"].view(-1, p.l)
-        idx = self.torch.as_tensor(slots, device=self.dev, dtype=self.torch.int64)
-        return dig.index_select(0, idx).reshape(-1).contiguous()
+        if getattr(self, "_halo_t", None) is None:
+            self._halo_t = self.torch.zeros(p.Tr * p.H * p.l, dtype=self.torch.int64, device=self.dev)
+        return self._halo_t
 
-    def combine(self, sh, phase, m0, mcount, kbase, halo, H, cin):
-        t = self.torch
-        nb = self.mp.shard_combine_tmp_bytes(mcount)
-        if self._tmp is None or self._tmp.numel() < nb:
-            self._tmp = t.empty(nb, dtype=t.uint8, device=self.dev)
+    def cat(self, views):
+        return self.torch.cat(views)
+
+    def combine(self, sh, phase, halo, sums_all=None):
+        """phase 0: (stripes, summaries) with carry-in 0; phase 1: each stripe's carry-in from
+        every rank's summaries (a list, rank order)"""
+        t, p = self.torch, self.p
+        if self._tmp is None:
+            nb = self.mp.shard_combine_tmp_bytes(p.n1, p.n2, p.depth, p.w, p.world)
+            self._tmp = t.empty(max(nb, 1), dtype=t.uint8, device=self.dev)
+            self._r = t.empty(p.Tr * p.SL, dtype=t.int64, device=self.dev)
+            self._sums = t.zeros(2 * p.Tr, dtype=t.int32, device=self.dev)
+        desc = self._desc(sh)
         if phase == 0:
-            self._sum = t.zeros(2, dtype=t.int32, device=self.dev)
-            self._r = t.empty(mcount, dtype=t.int64, device=self.dev)
-            halo_d = halo.to(self.dev) if halo is not None else None
-            self._halo = halo_d
-            self.mp.shard_combine(self._desc(sh), 0, self._r, m0, mcount, kbase, halo_d, H, self._tmp, cin,
-                                  self._sum, self.stream)
-            return self._sum
-        self.mp.shard_combine(self._desc(sh), 1, self._r, m0, mcount, kbase, self._halo, H, self._tmp, cin,
-                              self._sum, self.stream)
+            self.mp.shard_combine(desc, 0, self._r, halo, self._sums, None, self._tmp, self.stream)
+            return self._r, self._sums
+        allv = t.cat([x.to(self.dev) for x in sums_all])
+        self.mp.shard_combine(desc, 1, self._r, halo, self._sums, allv, self._tmp, self.stream)
         return self._r
 
 
@@ -487,7 +525,7 @@ def bench(args, cfg_name, cfg, rank, world, dev):
     sync_all()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        m0, limbs = job.run(da, db)
+        limbs = job.run(da, db)
     sync_all()
     el = max_over_ranks(time.perf_counter() - t0)
 
@@ -529,29 +567,28 @@ def bench(args, cfg_name, cfg, rank, world, dev):
             "note": "the slowest rank's dominant phase (all of its launches) vs one GPU's HBM peak; "
                     "algorithmic bytes = the phase's whole-multiply bytes / world"}
 
-    # end to end from host operands: this rank's column slices H2D, the multiply, its limbs D2H
+    # end to end from host operands: this rank's column slices H2D, the multiply, its stripes D2H
     sync_all()
     t1 = time.perf_counter()
     ea = torch.from_numpy(ha.view(np.int64)).to(dev)
     eb = torch.from_numpy(hb.view(np.int64)).to(dev)
-    _, el2 = job.run(ea, eb)
+    el2 = job.run(ea, eb)
     host_limbs = el2.cpu()
     sync_all()
     e2e_ms = max_over_ranks(time.perf_counter() - t1) * 1e3
     del ea, eb, host_limbs
 
-    # exactness: rank 0 gathers the limb ranges in rank order and hashes them (golden digest)
+    # exactness: rank 0 gathers every rank's stripes, puts them in order and hashes them
     exact = None
     if not getattr(args, "no_check", False):
         if rank == 0:
             parts = [limbs.cpu().numpy().view(np.uint64)]
             for d in range(1, world):
-                buf = torch.empty(plan.M[d + 1] - plan.M[d], dtype=torch.int64, device=dev if rccl else "cpu")
+                buf = torch.empty(plan.Tr * plan.SL, dtype=torch.int64, device=dev if rccl else "cpu")
                 dist.recv(buf, src=d)
                 parts.append(buf.cpu().numpy().view(np.uint64))
-            h = hashlib.sha256()
-            for p_ in parts:
-                h.update(p_.tobytes())
+            prod = plan.assemble(parts)
+            h = hashlib.sha256(prod.tobytes())
             gp = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
                               "products.json")
             try:
@@ -578,9 +615,9 @@ def bench(args, cfg_name, cfg, rank, world, dev):
                                    f"(l={P['l']}, NC x NR = {P['NC']} x {P['NR']}, trunc={P['trunc']})",
                        "parallelism": (f"MFA columns x{world}, " + (
                                 "forward columns replicated (whole operands on every rank), exchange #1 local; "
-                                "2 batched point-to-point exchanges" if rep else
-                                "operand column slices, 3 batched point-to-point exchanges") +
-                                f" + halo all-gather ({comm_label})"),
+                                "1 batched point-to-point exchange" if rep else
+                                "operand column slices, 2 batched point-to-point exchanges") +
+                                f" + per-stripe halo + summary all-gather, combine in the column layout ({comm_label})"),
                        "row_fused": job.fused},
             "roofline": roof,
             "phases_ms": phase_ms,
@@ -591,7 +628,7 @@ def bench(args, cfg_name, cfg, rank, world, dev):
                              "note": "timed on the N = 1 line only (rank 0, bounded sample: the bench contract); "
                                      "see BENCH_rNN.json cpu_baseline"},
             "e2e_host": {"ms": e2e_ms, "limbs_per_s": 2 * nl / (e2e_ms * 1e-3),
-                         "note": "per rank: its operands (column slices, or whole when replicated) H2D, the multiply, its product limbs D2H "
+                         "note": "per rank: its operands (column slices, or whole when replicated) H2D, the multiply, its product stripes D2H "
                                  "(host slicing excluded); max over ranks"},
             "exact": exact}
 

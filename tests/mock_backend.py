@@ -198,58 +198,74 @@ class MockBackend:
         self._itft1(x, off + h, h, t - h)
         self._pair(x, "ibfly", off, h, 0, t - h, self._rho(m))
 
-    # ---- combine -------------------------------------------------------
-    def _coef(self, sh, k, kbase, halo, H):
+    # ---- combine (column layout, stripes) --------------------------------
+    def halo_buffer(self):
+        p = self.p
+        return torch.zeros(p.Tr * p.H * p.l, dtype=torch.int64)
+
+    @staticmethod
+    def cat(views):
+        return torch.cat(views)
+
+    def _coef(self, sh, j, kbase, k, halo):
         p = self.p
         if k < kbase:
-            i = k - (kbase - H)
+            i = j * p.H + k - (kbase - p.H)
             limbs = halo[i * p.l:(i + 1) * p.l].numpy().view(np.uint64)
             return int.from_bytes(limbs.tobytes(), "little")
-        pl, c = k // p.NC - sh["r0"], k % p.NC
-        return self.get(sh["row"][0], self.row_slot(sh, pl, c))
+        assert k < kbase + p.C, "a stripe read past its own coefficients"
+        return self.get(sh["col"][0], self.col_slot(sh, j, k - kbase))
 
-    def tail_coeffs(self, sh, H):
-        p = self.p
-        end = (sh["r0"] + sh["rcount"]) * p.NC
-        out = torch.zeros(H * p.l, dtype=torch.int64)
-        for i, k in enumerate(range(end - H, end)):
-            pl, c = k // p.NC - sh["r0"], k % p.NC
-            s = self.row_slot(sh, pl, c)
-            out[i * p.l:(i + 1) * p.l] = sh["row"][0]["dig"][s * p.l:(s + 1) * p.l]
-        return out
-
-    def combine(self, sh, phase, m0, mcount, kbase, halo, H, cin):
-        """same window-sum / carry semantics as k_comb_sum + k_carry_* (kernels.hpp)"""
+    def combine(self, sh, phase, halo, sums_all=None):
+        """same window-sum / carry semantics as k_combine1 / k_comb_summary / k_stripe_carry
+        (combine.hpp): stripe j of rank g is product stripe j G + g"""
         p = self.p
         M64 = (1 << 64) - 1
-        lo, hi = [], []
-        for i in range(mcount + 1):
-            m = m0 - 1 + i
-            if m < 0:
-                lo.append(0)
-                hi.append(0)
-                continue
-            P = 64 * m
-            klo = (P - p.N) // p.bits1 if P >= p.N else 0
-            khi = min((P + 63) // p.bits1, p.len - 1)
-            sw = 0
-            for k in range(klo, khi + 1):
-                st = k * p.bits1
-                cv = self._coef(sh, k, kbase, halo, H)
-                sw += ((cv << (st - P)) if st > P else (cv >> (P - st))) & M64
-            lo.append(sw & M64)
-            hi.append(sw >> 64)
-        e = [lo[i + 1] + hi[i] for i in range(mcount)]
+        G, g = p.world, sh["c0"] // p.C
         if phase == 0:
-            run = 0
-            for v in e:
-                run = 1 if (v + run) > M64 else 0
-            allp = all(v == M64 for v in e)
-            return torch.tensor([run, 1 if allp else 0], dtype=torch.int32)
-        out, run = [], cin
-        for v in e:
-            t = v + run
-            out.append(t & M64)
-            run = t >> 64
-        arr = np.array(out, dtype=np.uint64).view(np.int64)
-        return torch.from_numpy(arr.copy())
+            self._r = torch.zeros(p.Tr * p.SL, dtype=torch.int64)
+            sums = []
+            for j in range(p.Tr):
+                s = j * G + g
+                m0, m1, kbase = p.ms[s], p.ms[s + 1], s * p.C
+                lo, hi = [], []
+                for m in range(m0 - 1, m1):
+                    if m < 0 or m1 == m0:
+                        lo.append(0)
+                        hi.append(0)
+                        continue
+                    P = 64 * m
+                    klo = (P - p.N) // p.bits1 + 1 if P >= p.N else 0
+                    khi = min((P + 63) // p.bits1, p.len - 1)
+                    sw = 0
+                    for k in range(klo, khi + 1):
+                        st = k * p.bits1
+                        cv = self._coef(sh, j, kbase, k, halo)
+                        sw += ((cv << (st - P)) if st > P else (cv >> (P - st))) & M64
+                    lo.append(sw & M64)
+                    hi.append(sw >> 64)
+                e = [lo[i + 1] + hi[i] for i in range(m1 - m0)]
+                run, out = 0, []
+                for v in e:
+                    t = v + run
+                    out.append(t & M64)
+                    run = t >> 64
+                if out:
+                    arr = np.array(out, dtype=np.uint64).view(np.int64)
+                    self._r[j * p.SL: j * p.SL + len(out)] = torch.from_numpy(arr.copy())
+                sums += [run, 1 if all(v == M64 for v in e) else 0]
+            return self._r, torch.tensor(sums, dtype=torch.int32)
+        allv = torch.cat(list(sums_all)).tolist()
+        for j in range(p.Tr):
+            s = j * G + g
+            cin = 0
+            for q in range(s):   # stripes below s in product order ([rank][j] layout)
+                e = (q % G) * p.Tr + q // G
+                cin = 1 if (allv[2 * e] or (allv[2 * e + 1] and cin)) else 0
+            if cin:
+                n = p.ms[s + 1] - p.ms[s]
+                v = int.from_bytes(self._r[j * p.SL: j * p.SL + n].numpy().view(np.uint64).tobytes(), "little") + 1
+                v &= (1 << (64 * n)) - 1
+                arr = np.frombuffer(v.to_bytes(8 * n, "little"), dtype=np.uint64).view(np.int64)
+                self._r[j * p.SL: j * p.SL + n] = torch.from_numpy(arr.copy())
+        return self._r

@@ -1,9 +1,11 @@
-"""GPU tests of the one-process multi-GPU entry mpfft_mul_multi (csrc/multi.hip) and the
-new_mpn_mul device policy (mpfft_set_devices).  On the one-GPU box every rank is placed on
-device 0: the ranks' stages, the three exchanges (same-device copies instead of xGMI peer
-DMA -- the copy plan, offsets and event ordering are the same), the halo and the cross-rank
-carry scan run exactly as on eight GPUs.  C4 (BASELINE configs[4], 10^10 bits) at world 8
-is checked against its committed GMP digest."""
+"""GPU tests of the one-process multi-GPU entries mpfft_mul_multi / mpfft_mul_multi_device
+(csrc/multi.hip) and the new_mpn_mul device policy (mpfft_set_devices).  On the one-GPU box
+every rank is placed on device 0: the ranks' stages, the two exchanges (same-device copies
+instead of xGMI peer DMA -- the copy plan, offsets and event ordering are the same), the
+per-stripe halo, the striped combine and the device-side stripe carry scan run exactly as on
+eight GPUs.  C4 (BASELINE configs[4], 10^10 bits) at world 8 and 2 is checked against its
+committed GMP digest.  The cross-device peer path itself (hipMemcpyPeerAsync between distinct
+GPUs) has not run on separate GPUs from these tests."""
 import hashlib
 import json
 import os
@@ -43,6 +45,44 @@ def test_mul_multi_column_policy_forced(mp, oracle, monkeypatch, world, rep, dep
     assert (mp.mul_multi(a, b, depth, w, [0] * world) == oracle.gmp_mul(a, b)).all()
 
 
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+@pytest.mark.parametrize("depth,w,n", [(13, 32, 1000000), (15, 4, 2000000), (10, 1, 2000)])
+def test_mul_multi_all_ones(mp, oracle, world, depth, w, n):
+    """all-ones operands: the product's upper half is all-ones limbs, so carries cross stripe
+    and rank boundaries and k_stripe_carry decides them"""
+    a = np.full(n, (1 << 64) - 1, dtype=np.uint64)
+    assert (mp.mul_multi(a, a, depth, w, [0] * world) == oracle.gmp_mul(a, a)).all()
+
+
+@pytest.mark.parametrize("world", [1, 2, 8])
+@pytest.mark.parametrize("depth,w,n1,n2", [(13, 32, 1000000, 999000), (15, 4, 2000000, 1900000)])
+def test_mul_multi_device_entry(mp, oracle, world, depth, w, n1, n2):
+    """mpfft_mul_multi_device: packed operand slices already on the devices (mpfft_shard_pack),
+    stripes back on the devices, ordered on the callers' torch streams; twice (the second call
+    queued behind the first on the same streams)"""
+    import torch
+    dev = torch.device("cuda:0")
+    a = mp.fill_random(n1, 0x51 + world)
+    b = mp.fill_random(n2, 0x62 + world)
+    part = mp.shard_partition(n1, n2, depth, w, world)
+    src1 = [torch.from_numpy(mp.shard_pack(a, n1, n2, depth, w, world, g).view(np.int64)).to(dev) for g in range(world)]
+    src2 = [torch.from_numpy(mp.shard_pack(b, n1, n2, depth, w, world, g).view(np.int64)).to(dev) for g in range(world)]
+    outs = [torch.empty(part["Tr"] * part["SL"], dtype=torch.int64, device=dev) for _ in range(world)]
+    st = torch.cuda.Stream(dev)
+    want = oracle.gmp_mul(a, b)
+    for _ in range(2):
+        with torch.cuda.stream(st):
+            for o in outs:
+                o.fill_(-1)
+            mp.mul_multi_device(n1, n2, depth, w, [0] * world, src1, src2, outs, streams=[st] * world)
+        st.synchronize()
+        got = mp.assemble_stripes(part, world, [o.cpu().numpy().view(np.uint64) for o in outs])
+        assert (got == want).all()
+    mp.mul_multi_device(n1, n2, depth, w, [0] * world, src1, src2, outs)   # streams=None: synchronous
+    got = mp.assemble_stripes(part, world, [o.cpu().numpy().view(np.uint64) for o in outs])
+    assert (got == want).all()
+
+
 def test_mul_multi_c4_world2_digest(mp):
     """C4 over two ranks on device 0 with the default (replicated) forward columns, against the
     GMP digest"""
@@ -59,8 +99,8 @@ def test_mul_multi_c4_world2_digest(mp):
 
 def test_mul_multi_c4_world8_digest(mp):
     """C4 split 8 ways exactly as on an 8-GPU node (the plan's columns and live rows dealt evenly
-    over 8 ranks, seven-peer exchanges, halo, carry scan) with all ranks on device 0,
-    against the GMP digest."""
+    over 8 ranks, seven-peer exchanges, per-stripe halo, stripe carry scan) with all ranks on
+    device 0, against the GMP digest."""
     with open(os.path.join(HERE, "golden", "products.json")) as f:
         case = {c["name"]: c for c in json.load(f)}["C4"]
     n1, n2, depth, w = case["n1"], case["n2"], case["depth"], case["w"]

@@ -38,10 +38,10 @@ def test_sharded_world1(mp, oracle, depth, w, n1, n2):
     da, db = torch.from_numpy(sa.view(np.int64)).to(dev), torch.from_numpy(sb.view(np.int64)).to(dev)
     want = oracle.gmp_mul(a, b)
     for run in range(2):
-        m0, limbs = job.run(da, db)
+        limbs = job.run(da, db)
         torch.cuda.synchronize()
-        got = limbs.cpu().numpy().view(np.uint64)
-        assert m0 == 0 and (got == want).all(), run
+        got = plan.assemble([limbs.cpu().numpy().view(np.uint64)])
+        assert (got == want).all(), run
         for k in range(2):   # world 1: every row array is a view of its column array
             assert job.row[k]["dig"].data_ptr() == job.col[k]["dig"].data_ptr()
 
@@ -49,7 +49,7 @@ def test_sharded_world1(mp, oracle, depth, w, n1, n2):
 def test_sharded_world1_c4_digest(mp):
     """BASELINE configs[4] (10^10-bit, depth 17, w 2, l = 4096) through the column-sharded
     code path at world 1 -- operand column slices, the fused-split loaders at l = 4096, the
-    local exchanges and the rank combine -- against the committed GMP digest of C4."""
+    local exchanges, the halo and the striped combine -- against the committed GMP digest of C4."""
     import hashlib
     import json
     import torch
@@ -67,10 +67,10 @@ def test_sharded_world1_c4_digest(mp):
     del b
     job = ShardedMul(plan, 0, GpuBackend(mp, plan, dev), _SoloComm())
     for run in range(2):   # the second run on swapped (still aliased) arrays
-        m0, limbs = job.run(sa, sb)
+        limbs = job.run(sa, sb)
         torch.cuda.synchronize()
-        got = limbs.cpu().numpy().view(np.uint64)
-        assert m0 == 0 and len(got) == 2 * nl
+        got = plan.assemble([limbs.cpu().numpy().view(np.uint64)])
+        assert len(got) == 2 * nl
         assert hashlib.sha256(got.tobytes()).hexdigest() == want["sha256"], run
         del got
     del job, sa, sb, limbs
@@ -109,16 +109,13 @@ def _worker(rank, world, port, depth, w, n1, n2, q, replicate=False):
             sa, sb = a, b
         else:
             sa, sb = plan.slice_operand(a, rank), plan.slice_operand(b, rank)   # this rank's column slices
-        m0, limbs = job.run(torch.from_numpy(sa.view(np.int64)).to(dev), torch.from_numpy(sb.view(np.int64)).to(dev))
+        limbs = job.run(torch.from_numpy(sa.view(np.int64)).to(dev), torch.from_numpy(sb.view(np.int64)).to(dev))
         limbs = limbs.cpu()
-        sizes = [plan.M[d + 1] - plan.M[d] for d in range(world)]
-        pad = torch.zeros(max(sizes), dtype=torch.int64)
-        pad[: limbs.numel()] = limbs
-        bufs = [torch.zeros(max(sizes), dtype=torch.int64) for _ in range(world)]
-        dist.all_gather(bufs, pad)
+        bufs = [torch.zeros_like(limbs) for _ in range(world)]
+        dist.all_gather(bufs, limbs)
         if rank == 0:
             import oracle as O
-            prod = np.concatenate([bufs[d][: sizes[d]].numpy() for d in range(world)]).view(np.uint64)
+            prod = plan.assemble([x.numpy().view(np.uint64) for x in bufs])
             q.put("ok" if (prod == O.gmp_mul(a, b)).all() else "mismatch")
     except Exception as e:  # pragma: no cover
         q.put("error " + repr(e))
