@@ -265,6 +265,7 @@ struct Rank {
     void *tmp = nullptr;
     size_t tmp_bytes = 0;
     const u64 *in[2] = {nullptr, nullptr};   // this call's operand slices
+    bool whole = false;                      // ... or the whole operands (host entry, replicated columns)
     u64 *out = nullptr;                      // this call's product stripes
     u64 *hsend = nullptr, *hstage = nullptr;  // the halo's send block and staging (HaloRank)
     Run *d_pack = nullptr, *d_scatter = nullptr;   // its run tables on the device
@@ -331,8 +332,10 @@ int setup_rank(const Part &p, int d, Rank &R, bool host, const HaloRank &HR)
     const int nrow = w1 ? 0 : (p.fused ? 3 : 2);      // world 1: row arrays are views
     auto arr_bytes = [&](long slots) { return al(slots * p.l * 8) + al(slots * p.cbw * 8) + al(slots * 4); };
     const size_t ctb = mpfft_shard_combine_tmp_bytes(p.n1, p.n2, p.depth, p.w, p.world);
-    const long sl = p.src_limbs();                    // operand slices held (all blocks' when replicated)
-    const size_t need = ncol * arr_bytes(cs) + nrow * arr_bytes(rs) + (host ? 2 * al(sl * 8) + al(p.Tr * p.SL * 8) : 0) +
+    // the host entry's device copies of its operands: the rank's slices, or the whole operands
+    // when every rank computes every column block (no packing: straight H2D)
+    const long s1 = p.rep ? p.n1 : p.src_limbs(), s2 = p.rep ? p.n2 : p.src_limbs();
+    const size_t need = ncol * arr_bytes(cs) + nrow * arr_bytes(rs) + (host ? al(s1 * 8) + al(s2 * 8) + al(p.Tr * p.SL * 8) : 0) +
                         al(p.Tr * p.H * p.l * 8) + al(p.Tr * 2 * 4) + al(p.world * p.Tr * 2 * 4) + al(ctb) +
                         al(HR.send_n * 8) + al(HR.stage_n * 8) + al(HR.pack.size() * sizeof(Run)) +
                         al(HR.scatter.size() * sizeof(Run)) + 256;
@@ -391,10 +394,11 @@ int setup_rank(const Part &p, int d, Rank &R, bool host, const HaloRank &HR)
         R.tables_key = key;
     }
     if (host) {
-        R.src[0] = (u64 *)q; q += al(sl * 8);
-        R.src[1] = (u64 *)q; q += al(sl * 8);
+        R.src[0] = (u64 *)q; q += al(s1 * 8);
+        R.src[1] = (u64 *)q; q += al(s2 * 8);
         R.r = (u64 *)q; q += al(p.Tr * p.SL * 8);
-        const size_t hb = (size_t)2 * sl * 8;
+        // pinned staging: the packed slices on the way in, the stripes on the way out
+        const size_t hb = (size_t)std::max<long>(p.rep ? 0 : 2 * p.src_limbs(), p.Tr * p.SL) * 8;
         if (R.host_bytes < hb) {
             if (R.host) MCHK(hipHostFree(R.host));
             R.host = nullptr;
@@ -433,7 +437,7 @@ mpfft_shard desc(const Part &p, int d, const Rank &R, unsigned long depth, unsig
         sh.row_cb[k] = R.row[k].cb;
         sh.row_top[k] = R.row[k].top;
     }
-    sh.src_chunk = p.chunk;
+    sh.src_chunk = R.whole ? 0 : p.chunk;
     if (p.fused) {
         sh.rowc_dig = R.rowc.dig;
         sh.rowc_cb = R.rowc.cb;
@@ -502,7 +506,8 @@ int fwd_replicated(const Part &p, std::vector<Rank> &rk, unsigned long depth, un
         for (int e = 0; e < p.world; ++e) {
             mpfft_shard sh = desc(p, d, R, depth, w);
             sh.c0 = (int)(e * p.C);
-            int rc = mpfft_shard_stage(MPFFT_SHARD_FWD_COLUMNS, &sh, R.in[0] + e * sl, R.in[1] + e * sl, R.s);
+            const long o = R.whole ? 0 : e * sl;   // block e's slices, or the whole operands
+            int rc = mpfft_shard_stage(MPFFT_SHARD_FWD_COLUMNS, &sh, R.in[0] + o, R.in[1] + o, R.s);
             if (rc) return rc;
             for (const mpfft_copy &c : plan)
                 if (c.dst == d && c.src == e) {
@@ -723,18 +728,26 @@ int mul_multi_locked(Ctx &X, uint64_t *r1, const uint64_t *i1, long n1, const ui
     if ((rc = prepare(X, p, devs, true))) return rc;
     std::vector<Rank> &rk = X.ranks;
 
-    // operand slices: packed and copied by one host thread per rank
+    // operands in: the whole operands straight from the caller's arrays when every rank
+    // computes every column block (replicated), else each rank's slices packed into its pinned
+    // staging; one host thread per rank
     std::vector<int> trc(G, MPFFT_OK);
     {
         std::vector<std::thread> th;
         for (int d = 0; d < G; ++d)
             th.emplace_back([&, d] {
                 Rank &R = rk[d];
+                if (hipSetDevice(R.dev) != hipSuccess) { trc[d] = MPFFT_EHIP; return; }
+                if (p.rep) {
+                    if (hipMemcpyAsync(R.src[0], i1, (size_t)n1 * 8, hipMemcpyHostToDevice, R.s) != hipSuccess ||
+                        hipMemcpyAsync(R.src[1], i2, (size_t)n2 * 8, hipMemcpyHostToDevice, R.s) != hipSuccess)
+                        trc[d] = MPFFT_EHIP;
+                    return;
+                }
                 const long sl = p.src_limbs();
                 pack_slices(p, d, i1, n1, R.host);
                 pack_slices(p, d, i2, n2, R.host + sl);
-                if (hipSetDevice(R.dev) != hipSuccess ||
-                    hipMemcpyAsync(R.src[0], R.host, (size_t)sl * 8, hipMemcpyHostToDevice, R.s) != hipSuccess ||
+                if (hipMemcpyAsync(R.src[0], R.host, (size_t)sl * 8, hipMemcpyHostToDevice, R.s) != hipSuccess ||
                     hipMemcpyAsync(R.src[1], R.host + sl, (size_t)sl * 8, hipMemcpyHostToDevice, R.s) != hipSuccess)
                     trc[d] = MPFFT_EHIP;
             });
@@ -745,23 +758,29 @@ int mul_multi_locked(Ctx &X, uint64_t *r1, const uint64_t *i1, long n1, const ui
     for (int d = 0; d < G; ++d) {
         rk[d].in[0] = rk[d].src[0];
         rk[d].in[1] = rk[d].src[1];
+        rk[d].whole = p.rep;
         rk[d].out = rk[d].r;
     }
-    if ((rc = run_ranks(p, rk, X.halo, depth, w))) return rc;
-    // product stripes into their places in r1: one thread per rank (pageable destination)
+    rc = run_ranks(p, rk, X.halo, depth, w);
+    for (int d = 0; d < G; ++d) rk[d].whole = false;
+    if (rc) return rc;
+    // product stripes out: per rank one D2H of its stripe buffer into its pinned staging, then
+    // the stripes copied into their places in r1 (one host thread per rank)
     {
         std::vector<std::thread> th;
         for (int d = 0; d < G; ++d)
             th.emplace_back([&, d] {
                 Rank &R = rk[d];
-                if (hipSetDevice(R.dev) != hipSuccess) { trc[d] = MPFFT_EHIP; return; }
-                for (long j = 0; j < p.Tr && !trc[d]; ++j) {
-                    const long s = j * G + d, cnt = p.ms[s + 1] - p.ms[s];
-                    if (cnt > 0 && hipMemcpyAsync(r1 + p.ms[s], R.r + j * p.SL, (size_t)cnt * 8, hipMemcpyDeviceToHost,
-                                                  R.s) != hipSuccess)
-                        trc[d] = MPFFT_EHIP;
+                if (hipSetDevice(R.dev) != hipSuccess ||
+                    hipMemcpyAsync(R.host, R.r, (size_t)p.Tr * p.SL * 8, hipMemcpyDeviceToHost, R.s) != hipSuccess ||
+                    hipStreamSynchronize(R.s) != hipSuccess) {
+                    trc[d] = MPFFT_EHIP;
+                    return;
                 }
-                if (hipStreamSynchronize(R.s) != hipSuccess) trc[d] = MPFFT_EHIP;
+                for (long j = 0; j < p.Tr; ++j) {
+                    const long s = j * G + d, cnt = p.ms[s + 1] - p.ms[s];
+                    if (cnt > 0) memcpy(r1 + p.ms[s], R.host + j * p.SL, (size_t)cnt * 8);
+                }
             });
         for (auto &t : th) t.join();
         for (int d = 0; d < G; ++d)

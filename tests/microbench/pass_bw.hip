@@ -24,11 +24,25 @@ __global__ __launch_bounds__(256) void k_stream(v4u *x, long n16)
     }
 }
 
+// out-of-place streaming (ping-pong passes): read x, write y
+__global__ __launch_bounds__(256) void k_stream_oop(const v4u *x, v4u *y, long n16)
+{
+    const long nt = (long)gridDim.x * blockDim.x;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += 4 * nt) {
+        v4u v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = i + k * nt < n16 ? x[i + k * nt] : v4u{0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (i + k * nt < n16) y[i + k * nt] = v[k] + 1u;
+    }
+}
+
 // one workgroup = one group of G coefficients of L limbs at stride S coefficients (a column
 // pass: positions pos0 + i * S); NT threads, each 16 B x (L / 2 / NT) per coefficient.
 // LDS: `lds` bytes of dummy allocation (k_rpass: 74 KB at l = 2048, G = 8 -> 2 WGs per CU).
 template <int G, int NT, int L>
-__global__ __launch_bounds__(NT) void k_group(v4u *x, int stride, int ngroups_per_col, int spin)
+__global__ __launch_bounds__(NT) void k_group(v4u *x, int stride, int ngroups_per_col, int spin, v4u *y = nullptr)
 {
     extern __shared__ unsigned char smem[];
     constexpr int R = L / 2 / NT;
@@ -55,7 +69,7 @@ __global__ __launch_bounds__(NT) void k_group(v4u *x, int stride, int ngroups_pe
     for (int i = 0; i < G; ++i) {
         const long slot = (long)(grp + i * ngroups_per_col) * stride + col;
 #pragma unroll
-        for (int r = 0; r < R; ++r) x[slot * (L / 2) + t + NT * r] = v[i][r] + 1u;
+        for (int r = 0; r < R; ++r) (y ? y : x)[slot * (L / 2) + t + NT * r] = v[i][r] + 1u;
     }
 }
 
@@ -96,9 +110,9 @@ int main()
         for (int spin : {0, 64, 256}) {
             auto f = k_group<8, 512, 2048>;
             if (lds > 64 * 1024) CHK(hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-            hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(512), lds, 0, x, ncols, gpc, spin);
+            hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(512), lds, 0, x, ncols, gpc, spin, (v4u *)nullptr);
             CHK(hipEventRecord(e0));
-            for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(512), lds, 0, x, ncols, gpc, spin);
+            for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(512), lds, 0, x, ncols, gpc, spin, (v4u *)nullptr);
             CHK(hipEventRecord(e1));
             CHK(hipEventSynchronize(e1));
             float ms;
@@ -112,9 +126,9 @@ int main()
         auto f = k_group<8, 1024, 2048>;
         const int lds = 74 * 1024;
         CHK(hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(1024), lds, 0, x, ncols, gpc, spin);
+        hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(1024), lds, 0, x, ncols, gpc, spin, (v4u *)nullptr);
         CHK(hipEventRecord(e0));
-        for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(1024), lds, 0, x, ncols, gpc, spin);
+        for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(1024), lds, 0, x, ncols, gpc, spin, (v4u *)nullptr);
         CHK(hipEventRecord(e1));
         CHK(hipEventSynchronize(e1));
         float ms;
@@ -123,12 +137,66 @@ int main()
         snprintf(nm, sizeof nm, "group G=8 NT=1024 lds=74K spin=%d", spin);
         report(nm, ms, reps);
     }
+    // out of place (round 5): the same shapes reading x and writing a second
+    // array y, i.e. column passes ping-ponging between two halves of a doubled array
+    v4u *y;
+    CHK(hipMalloc(&y, bytes));
+    CHK(hipMemset(y, 2, bytes));
+    {
+        const long n16 = bytes / 16;
+        for (int grid : {1024, 2048, 4096}) {
+            hipLaunchKernelGGL(k_stream_oop, dim3(grid), dim3(256), 0, 0, x, y, n16);
+            CHK(hipEventRecord(e0));
+            for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(k_stream_oop, dim3(grid), dim3(256), 0, 0, x, y, n16);
+            CHK(hipEventRecord(e1));
+            CHK(hipEventSynchronize(e1));
+            float ms;
+            CHK(hipEventElapsedTime(&ms, e0, e1));
+            char nm[64];
+            snprintf(nm, sizeof nm, "stream out of place, grid %d x 256", grid);
+            report(nm, ms, reps);
+        }
+    }
+    for (int oop : {0, 1}) {
+        for (int spin : {0, 16, 64}) {   // the four-level pass's shape: G = 16, NT = 1024, 148 KB LDS, one WG per CU
+            auto f = k_group<16, 1024, 2048>;
+            const int lds = 148 * 1024, gpc16 = (int)(NPOS / 16);
+            CHK(hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+            hipLaunchKernelGGL(f, dim3(ncols * gpc16), dim3(1024), lds, 0, x, ncols, gpc16, spin, oop ? y : nullptr);
+            CHK(hipEventRecord(e0));
+            for (int i = 0; i < reps; ++i)
+                hipLaunchKernelGGL(f, dim3(ncols * gpc16), dim3(1024), lds, 0, x, ncols, gpc16, spin, oop ? y : nullptr);
+            CHK(hipEventRecord(e1));
+            CHK(hipEventSynchronize(e1));
+            float ms;
+            CHK(hipEventElapsedTime(&ms, e0, e1));
+            char nm[96];
+            snprintf(nm, sizeof nm, "group G=16 NT=1024 lds=148K spin=%d %s", spin, oop ? "out of place" : "in place");
+            report(nm, ms, reps);
+        }
+        for (int spin : {0, 64}) {   // the three-level pass's shape out of place
+            auto f = k_group<8, 512, 2048>;
+            const int lds = 74 * 1024;
+            CHK(hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+            hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(512), lds, 0, x, ncols, gpc, spin, oop ? y : nullptr);
+            CHK(hipEventRecord(e0));
+            for (int i = 0; i < reps; ++i)
+                hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(512), lds, 0, x, ncols, gpc, spin, oop ? y : nullptr);
+            CHK(hipEventRecord(e1));
+            CHK(hipEventSynchronize(e1));
+            float ms;
+            CHK(hipEventElapsedTime(&ms, e0, e1));
+            char nm[96];
+            snprintf(nm, sizeof nm, "group G=8 NT=512 lds=74K spin=%d %s", spin, oop ? "out of place" : "in place");
+            report(nm, ms, reps);
+        }
+    }
     for (int spin : {0, 64}) {   // G = 4 (two levels per pass), 4 WGs per CU
         auto f = k_group<4, 512, 2048>;
         const int lds = 37 * 1024;
-        hipLaunchKernelGGL(f, dim3(ncols * (NPOS / 4)), dim3(512), lds, 0, x, ncols, (int)(NPOS / 4), spin);
+        hipLaunchKernelGGL(f, dim3(ncols * (NPOS / 4)), dim3(512), lds, 0, x, ncols, (int)(NPOS / 4), spin, (v4u *)nullptr);
         CHK(hipEventRecord(e0));
-        for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(f, dim3(ncols * (NPOS / 4)), dim3(512), lds, 0, x, ncols, (int)(NPOS / 4), spin);
+        for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(f, dim3(ncols * (NPOS / 4)), dim3(512), lds, 0, x, ncols, (int)(NPOS / 4), spin, (v4u *)nullptr);
         CHK(hipEventRecord(e1));
         CHK(hipEventSynchronize(e1));
         float ms;
