@@ -377,8 +377,11 @@ def main():
         if world > 1:
             dist.barrier()
         res = sh.bench(args, cfg, CONFIGS[cfg], rank, world, dev)
+        # the other ranks wait on a host-side (gloo) barrier while rank 0 times the C entry on
+        # their devices: an RCCL barrier would leave a kernel spinning on each of those GPUs
+        host_pg = dist.new_group(backend="gloo") if world > 1 else None
         if world > 1:
-            dist.barrier()
+            dist.barrier(group=host_pg)
         if rank == 0:
             res["n1_twin"] = twin
             if not args.no_c_entry:
@@ -393,7 +396,7 @@ def main():
                     res["c_entry"] = {"error": repr(e)}
             print(json.dumps(res))
         if world > 1:
-            dist.barrier()
+            dist.barrier(group=host_pg)
             dist.destroy_process_group()
         return
 

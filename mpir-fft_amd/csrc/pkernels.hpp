@@ -259,10 +259,30 @@ __host__ __device__ __forceinline__ void pw_sqrt2(u64 (&L)[M], int &T)
     T = (int)(i64)(a1 + c);
 }
 
+// The product's limbs go to `Z`: registers (u64 (&)[M]) or, on the device, this thread's word
+// column of the LDS exchange rows (PwLdsZ: limb j as words 2j, 2j + 1) -- the latter keeps the M limbs out of the
+// registers while the 2 ND digits are live (the l = 4096 kernel spilled 32 VGPRs at the
+// 128-VGPR budget with the limbs in registers, the l = 2048 one 5).
+struct PwLdsRef {
+    u32 *p;    // word 0 of the limb (its high word K further): the publish layout (pw_publish_words)
+    int K;
+    __device__ __forceinline__ operator u64() const { return ((u64)p[K] << 32) | p[0]; }
+    __device__ __forceinline__ PwLdsRef &operator=(u64 v)
+    {
+        p[0] = (u32)v;
+        p[K] = (u32)(v >> 32);
+        return *this;
+    }
+};
+struct PwLdsZ {
+    u32 *z;    // Xw + t: this thread's own word column (the u64 rows would straddle two threads' columns)
+    int K;
+    __device__ __forceinline__ PwLdsRef operator[](int j) const { return PwLdsRef{z + 2 * j * K, K}; }
+};
+
 // z = a b mod p' for canonical a (La, ta), b (Lb, tb); result limbs + top (value = L + T 2^N')
-template <int M>
-__host__ __device__ __forceinline__ void pw_mulmod(u64 (&Z)[M], int &T, const u64 (&La)[M], int ta, const u64 (&Lb)[M],
-                                          int tb)
+template <int M, typename ZT>
+__host__ __device__ __forceinline__ void pw_mulmod(ZT &&Z, int &T, const u64 (&La)[M], int ta, const u64 (&Lb)[M], int tb)
 {
     if (ta | tb) {   // 2^N' == -1: the product is 1, -b or -a  (cf. mul_fft.c:3250)
         if (ta && tb) {
@@ -272,12 +292,10 @@ __host__ __device__ __forceinline__ void pw_mulmod(u64 (&Z)[M], int &T, const u6
             return;
         }
         // -v = ~v + 1 - 2^N'  ->  limbs ~v, +1 at limb 0, top -1
-#pragma unroll
-        for (int j = 0; j < M; ++j) Z[j] = ta ? Lb[j] : La[j];
         i128 acc = 1;
 #pragma unroll
         for (int j = 0; j < M; ++j) {
-            acc += (i128)(~Z[j]);
+            acc += (i128)(~(ta ? Lb[j] : La[j]));
             Z[j] = (u64)acc;
             acc >>= 64;
         }
@@ -345,10 +363,14 @@ template <int M, int LK>
 __device__ __forceinline__ void pw_publish_words(const u64 (&L)[M], u32 *Xw, int t)
 {
     constexpr int K = 1 << LK;
+    // (an opaque copy of this address, to keep the second base register of the rows past the
+    // 64 KiB ds offset reach from living across the levels, cut the l = 4096 spills 84 -> 68 B
+    // per lane and slowed the kernel 40.0 -> 44.5 ms: profiles/r05/pw_lds_product_ab.txt)
+    u32 *col = Xw + t;
 #pragma unroll
     for (int j = 0; j < M; ++j) {
-        Xw[(2 * j) * K + t] = (u32)L[j];
-        Xw[(2 * j + 1) * K + t] = (u32)(L[j] >> 32);
+        col[(2 * j) * K] = (u32)L[j];
+        col[(2 * j + 1) * K] = (u32)(L[j] >> 32);
     }
 }
 
@@ -669,7 +691,18 @@ __device__ __forceinline__ void pw_slot_product(u64 (&La)[M], int Ta, u64 (&Lb)[
     const int ca = pw_canon<M>(La, Ta), cb = pw_canon<M>(Lb, Tb);
     u64 Z[M];
     int Tz, Sz = Sa ^ Sb;
-    pw_mulmod<M>(Z, Tz, La, ca, Lb, cb);
+    if (pw_tight(K)) {
+        // the product's limbs through this thread's own LDS word column (B's transform ended
+        // with an in-wave level: no other wave reads this column; the inverse's first publish
+        // comes after): C4 pointwise 40.5 -> 40.0 ms, its spills 128 -> 84 B per lane; at
+        // l = 2048 (no spills either way) the register form is faster (3.57 vs 3.67 ms),
+        // profiles/r05/pw_lds_product_ab.txt
+        pw_mulmod<M>(PwLdsZ{Xw + t, K}, Tz, La, ca, Lb, cb);
+#pragma unroll
+        for (int j = 0; j < M; ++j) Z[j] = ((u64)Xw[(2 * j + 1) * K + t] << 32) | Xw[2 * j * K + t];
+    } else {
+        pw_mulmod<M>(Z, Tz, La, ca, Lb, cb);
+    }
     unsigned Pz = pw_mod(Pa + Pb, N2);
     PW_STAMP(4);
 

@@ -23,6 +23,21 @@ __global__ __launch_bounds__(256) void k_asm(const u32 *in, u64 *out, int iters)
     u64 s = 0; for (int c = 0; c < CH; ++c) s += acc[c] + h[c];
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
+__global__ __launch_bounds__(256) void k_mad(const u32 *in, u64 *out, int iters) {
+    u32 a[CH], b = in[threadIdx.x] | 1; u64 acc[CH];
+    for (int c = 0; c < CH; ++c) { a[c] = in[threadIdx.x + c + 1]; acc[c] = c; }
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            u64 cy;
+            asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc[c]), "=&s"(cy) : "v"(a[c]), "v"(b));
+            (void)cy;
+        }
+        b += 0x9e37;
+    }
+    u64 s = 0; for (int c = 0; c < CH; ++c) s += acc[c];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
 __global__ __launch_bounds__(256) void k_cc(const u32 *in, u64 *out, int iters) {
     u32 a[CH], b = in[threadIdx.x] | 1; u64 acc[CH]; u32 h[CH];
     for (int c = 0; c < CH; ++c) { a[c] = in[threadIdx.x + c + 1]; acc[c] = c; h[c] = 0; }
@@ -64,7 +79,7 @@ int main() {
     hipMemset(in, 0x5b, 4096 * 4);
     hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
     struct { const char *name; void (*k)(const u32*, u64*, int); double ops_per_iter; } ks[] = {
-        {"asm v_mad_u64_u32+v_addc (MAC)", k_asm, CH}, {"compiler u64 MAC", k_cc, CH},
+        {"asm v_mad_u64_u32+v_addc (MAC)", k_asm, CH}, {"asm v_mad_u64_u32 alone", k_mad, CH}, {"compiler u64 MAC", k_cc, CH},
         {"v_mul_lo+v_mul_hi (MAC halves)", k_mulhl, CH}, {"v_add_u32+xor (2 simple ops)", k_add, CH}};
     for (auto &k : ks) {
         for (int rep = 0; rep < 2; ++rep) {

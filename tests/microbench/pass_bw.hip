@@ -42,9 +42,17 @@ __global__ __launch_bounds__(256) void k_stream_oop(const v4u *x, v4u *y, long n
 // pass: positions pos0 + i * S); NT threads, each 16 B x (L / 2 / NT) per coefficient.
 // LDS: `lds` bytes of dummy allocation (k_rpass: 74 KB at l = 2048, G = 8 -> 2 WGs per CU).
 template <int G, int NT, int L>
-__global__ __launch_bounds__(NT) void k_group(v4u *x, int stride, int ngroups_per_col, int spin, v4u *y = nullptr)
+__global__ __launch_bounds__(NT) void k_group(v4u *x, int stride, int ngroups_per_col, int spin, v4u *y = nullptr,
+                                              int stagger = 0, int unit = 0)
 {
     extern __shared__ unsigned char smem[];
+    // stagger (round 5): the first workgroup on each CU waits (b mod stagger) units of ~3.4 us
+    // before its loads, so CUs that would otherwise load and compute in lockstep (identical
+    // groups started together) are spread over the period: while some compute, others load
+    if (stagger && blockIdx.x < 256) {
+        const int n = (int)(blockIdx.x % stagger) * unit;
+        for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+    }
     constexpr int R = L / 2 / NT;
     const int col = blockIdx.x / ngroups_per_col, grp = blockIdx.x % ngroups_per_col;
     const int t = threadIdx.x;
@@ -110,9 +118,9 @@ int main()
         for (int spin : {0, 64, 256}) {
             auto f = k_group<8, 512, 2048>;
             if (lds > 64 * 1024) CHK(hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-            hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(512), lds, 0, x, ncols, gpc, spin, (v4u *)nullptr);
+            hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(512), lds, 0, x, ncols, gpc, spin, (v4u *)nullptr, 0, 0);
             CHK(hipEventRecord(e0));
-            for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(512), lds, 0, x, ncols, gpc, spin, (v4u *)nullptr);
+            for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(512), lds, 0, x, ncols, gpc, spin, (v4u *)nullptr, 0, 0);
             CHK(hipEventRecord(e1));
             CHK(hipEventSynchronize(e1));
             float ms;
@@ -126,9 +134,9 @@ int main()
         auto f = k_group<8, 1024, 2048>;
         const int lds = 74 * 1024;
         CHK(hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(1024), lds, 0, x, ncols, gpc, spin, (v4u *)nullptr);
+        hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(1024), lds, 0, x, ncols, gpc, spin, (v4u *)nullptr, 0, 0);
         CHK(hipEventRecord(e0));
-        for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(1024), lds, 0, x, ncols, gpc, spin, (v4u *)nullptr);
+        for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(1024), lds, 0, x, ncols, gpc, spin, (v4u *)nullptr, 0, 0);
         CHK(hipEventRecord(e1));
         CHK(hipEventSynchronize(e1));
         float ms;
@@ -162,10 +170,10 @@ int main()
             auto f = k_group<16, 1024, 2048>;
             const int lds = 148 * 1024, gpc16 = (int)(NPOS / 16);
             CHK(hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-            hipLaunchKernelGGL(f, dim3(ncols * gpc16), dim3(1024), lds, 0, x, ncols, gpc16, spin, oop ? y : nullptr);
+            hipLaunchKernelGGL(f, dim3(ncols * gpc16), dim3(1024), lds, 0, x, ncols, gpc16, spin, oop ? y : nullptr, 0, 0);
             CHK(hipEventRecord(e0));
             for (int i = 0; i < reps; ++i)
-                hipLaunchKernelGGL(f, dim3(ncols * gpc16), dim3(1024), lds, 0, x, ncols, gpc16, spin, oop ? y : nullptr);
+                hipLaunchKernelGGL(f, dim3(ncols * gpc16), dim3(1024), lds, 0, x, ncols, gpc16, spin, oop ? y : nullptr, 0, 0);
             CHK(hipEventRecord(e1));
             CHK(hipEventSynchronize(e1));
             float ms;
@@ -178,10 +186,10 @@ int main()
             auto f = k_group<8, 512, 2048>;
             const int lds = 74 * 1024;
             CHK(hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-            hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(512), lds, 0, x, ncols, gpc, spin, oop ? y : nullptr);
+            hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(512), lds, 0, x, ncols, gpc, spin, oop ? y : nullptr, 0, 0);
             CHK(hipEventRecord(e0));
             for (int i = 0; i < reps; ++i)
-                hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(512), lds, 0, x, ncols, gpc, spin, oop ? y : nullptr);
+                hipLaunchKernelGGL(f, dim3(ncols * gpc), dim3(512), lds, 0, x, ncols, gpc, spin, oop ? y : nullptr, 0, 0);
             CHK(hipEventRecord(e1));
             CHK(hipEventSynchronize(e1));
             float ms;
@@ -191,12 +199,35 @@ int main()
             report(nm, ms, reps);
         }
     }
+    // staggered starts (round 5): the four-level shape with the levels' worth of compute
+    for (int spin : {16, 32, 64}) {
+        for (int st : {0, 2, 4, 8}) {
+            for (int unit : {1, 2, 4}) {
+                if (!st && unit > 1) continue;
+                auto f = k_group<16, 1024, 2048>;
+                const int lds = 148 * 1024, gpc16 = (int)(NPOS / 16);
+                CHK(hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+                hipLaunchKernelGGL(f, dim3(ncols * gpc16), dim3(1024), lds, 0, x, ncols, gpc16, spin, (v4u *)nullptr, st, unit);
+                CHK(hipEventRecord(e0));
+                for (int i = 0; i < reps; ++i)
+                    hipLaunchKernelGGL(f, dim3(ncols * gpc16), dim3(1024), lds, 0, x, ncols, gpc16, spin, (v4u *)nullptr, st,
+                                       unit);
+                CHK(hipEventRecord(e1));
+                CHK(hipEventSynchronize(e1));
+                float ms;
+                CHK(hipEventElapsedTime(&ms, e0, e1));
+                char nm[96];
+                snprintf(nm, sizeof nm, "G=16 NT=1024 148K spin=%d stagger=%d unit=%d", spin, st, unit);
+                report(nm, ms, reps);
+            }
+        }
+    }
     for (int spin : {0, 64}) {   // G = 4 (two levels per pass), 4 WGs per CU
         auto f = k_group<4, 512, 2048>;
         const int lds = 37 * 1024;
-        hipLaunchKernelGGL(f, dim3(ncols * (NPOS / 4)), dim3(512), lds, 0, x, ncols, (int)(NPOS / 4), spin, (v4u *)nullptr);
+        hipLaunchKernelGGL(f, dim3(ncols * (NPOS / 4)), dim3(512), lds, 0, x, ncols, (int)(NPOS / 4), spin, (v4u *)nullptr, 0, 0);
         CHK(hipEventRecord(e0));
-        for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(f, dim3(ncols * (NPOS / 4)), dim3(512), lds, 0, x, ncols, (int)(NPOS / 4), spin, (v4u *)nullptr);
+        for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(f, dim3(ncols * (NPOS / 4)), dim3(512), lds, 0, x, ncols, (int)(NPOS / 4), spin, (v4u *)nullptr, 0, 0);
         CHK(hipEventRecord(e1));
         CHK(hipEventSynchronize(e1));
         float ms;
