@@ -175,8 +175,9 @@ int mpfft_shard_combine(const mpfft_shard *sh, int phase, uint64_t *d_r, const u
 /* ---- multi-GPU from one C process (north_star: "host code stays C") ----------
  * The same column-sharded multiply as mpir-fft_amd/sharded.py (one process per GPU over
  * RCCL), driven from one host thread over G devices: every rank's stages on its own device
- * stream, the three exchanges as peer copies over xGMI (hipMemcpyPeerAsync; peer access
- * enabled between distinct devices), ordered by events.
+ * stream, the two exchanges and the halo as peer copies over xGMI (hipMemcpyPeerAsync; peer
+ * access enabled between distinct devices), ordered by events; the stripe carries on the device.
+ * (Tested with every rank on one device; the cross-device copies have not run on separate GPUs.)
  *
  * Partition of one multiply over `world` ranks (a power of two dividing the plan's NC,
  * out[2] of mpfft_plan_info -- at l = 2048 in truncation case b that is 2^(floor(depth/2)+1),
