@@ -151,6 +151,9 @@ int mpfft_shard_row_fused(long n1, long n2, unsigned long depth, unsigned long w
 #define MPFFT_SHARD_INV_COLUMNS 4   /* truncated column inverse + scale of A (column layout), canonical */
 #define MPFFT_SHARD_FWD_COLUMNS_A 5 /* MPFFT_SHARD_FWD_COLUMNS for operand 1 only (clears the combine flags) */
 #define MPFFT_SHARD_FWD_COLUMNS_B 6 /* ... for operand 2 only: with _A, lets operand 1's exchange overlap it */
+#define MPFFT_SHARD_FWD_COLUMNS_OWN 7 /* MPFFT_SHARD_FWD_COLUMNS, but only rows [r0, r0 + rcount) of the
+                                         column layout are computed (replicated forward columns: every
+                                         rank runs every column block for its own rows) */
 int mpfft_shard_stage(int stage, const mpfft_shard *sh, const uint64_t *d_i1, const uint64_t *d_i2, void *stream);
 /* The row stages (FWD_ROWS, POINTWISE, INV_ROWS) on local rows [lo, hi) of the shard only, so a
  * driver can run the row phase in chunks and start exchange #2 of a finished chunk early. */

@@ -416,7 +416,7 @@ __global__ __launch_bounds__(64 * BP_WAVES) void k_bpass(PassArgs a)
     const int lo = grp & ((1 << lobits) - 1);
     const int hi = grp >> lobits;
     const int bstart = hi << (a.lbM - a.lvl0);
-    if (DIR == 0 && bstart >= a.need) return;   // whole block past the truncation point (workgroup-uniform)
+    if (DIR == 0 && (bstart >= a.need || bstart + (1 << (a.lbM - a.lvl0)) <= a.need_lo)) return;   // whole block past the truncation point / outside the rows needed (workgroup-uniform)
     BGeo g;
     g.pos0 = bstart | lo;
     g.pstep = 1 << lobits;
@@ -609,7 +609,8 @@ __global__ __launch_bounds__(64 * BP_WAVES) void k_bpass(PassArgs a)
             const int t = t0 + q * nwv;
             if (t >= items) continue;
             const int i = t >> (lrows - 1), v = t & (bpr - 1);
-            const bool keep = DIR == 1 || ((g.pos0 + i * g.pstep) & ~(g.pstep - 1)) < a.need;
+            const int bs = (g.pos0 + i * g.pstep) & ~(g.pstep - 1);
+            const bool keep = DIR == 1 || (bs < a.need && bs + g.pstep > a.need_lo);
             if (!keep) continue;   // wave-uniform
             const long sl = wv_uniform(slot_of(i));
             const int m = 128 * v + 2 * lane;

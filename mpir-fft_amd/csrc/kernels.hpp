@@ -42,6 +42,8 @@ struct PassArgs {
     long jNC;            // fused split: coefficient index j = (pos_off + pos) * jNC + sub_off + sub
     int zero_from;       // forward: positions >= zero_from are zero inputs
     int need;            // forward: only blocks starting below `need` are live
+    int need_lo;         // forward: ... and ending above `need_lo` (a rank that needs only its own
+                         // rows of the columns: replicated forward columns, mpfft_shard_stage 7)
     int tw_mode;         // 1: pre-multiply by 2^(tw_w*pos*revbin(sub)), 2: post-multiply by its inverse
     u64 tw_w;
     int tw_lbR;
@@ -187,7 +189,7 @@ __global__ __launch_bounds__(MPF_LB(U)) void k_pass(PassArgs a)
     const int lo = grp & ((1 << lobits) - 1);
     const int hi = grp >> lobits;
     const int bstart = hi << (a.lbM - a.lvl0);
-    if (DIR == 0 && bstart >= a.need) return;  // whole block past the truncation point
+    if (DIR == 0 && (bstart >= a.need || bstart + (1 << (a.lbM - a.lvl0)) <= a.need_lo)) return;  // whole block past the truncation point / outside the rows needed
     const u64 N2 = 2 * a.N;
     // position of element i: pos0 + i * pstep
     const int pos0 = bstart | lo;
@@ -268,7 +270,8 @@ __global__ __launch_bounds__(MPF_LB(U)) void k_pass(PassArgs a)
 #pragma unroll
     for (int i = 0; i < G; ++i) {
         slot[i] = slot_of(i);
-        keep[i] = DIR == 1 || ((pos0 + i * pstep) & ~(pstep - 1)) < a.need;
+        const int bs = (pos0 + i * pstep) & ~(pstep - 1);
+        keep[i] = DIR == 1 || (bs < a.need && bs + pstep > a.need_lo);
     }
     normalize_store<U, G>(c, x, slot, keep, a.canon != 0, st, l, sm);
 }

@@ -119,7 +119,7 @@ __global__ __launch_bounds__(32 << LOGG) void k_lpass(PassArgs a)
     const int lo = grp & ((1 << lobits) - 1);
     const int hi = grp >> lobits;
     const int bstart = hi << (a.lbM - a.lvl0);
-    if (DIR == 0 && bstart >= a.need) return;   // whole block past the truncation point (workgroup-uniform)
+    if (DIR == 0 && (bstart >= a.need || bstart + (1 << (a.lbM - a.lvl0)) <= a.need_lo)) return;   // whole block past the truncation point / outside the rows needed (workgroup-uniform)
     const u64 N2 = 2 * a.N;
     const int pos0 = bstart | lo;
     const int pstep = 1 << lobits;
@@ -178,7 +178,8 @@ __global__ __launch_bounds__(32 << LOGG) void k_lpass(PassArgs a)
             }
             if (a.scale_e) e = lp_add(e, a.scale_e, N2);
         }
-        const bool keep = DIR == 1 || ((pos0 + i * pstep) & ~(pstep - 1)) < a.need;
+        const int bs = (pos0 + i * pstep) & ~(pstep - 1);
+        const bool keep = DIR == 1 || (bs < a.need && bs + pstep > a.need_lo);
         if (keep) {
             i64 x[2 * U];
             lp_read<U, F>(x, lds + (size_t)i * 2 * l, e, a.N, l, lane);

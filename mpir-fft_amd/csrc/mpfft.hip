@@ -364,6 +364,11 @@ struct Exec {
     int in_rows = 0;         // non-zero: inputs live in column rows [0, in_rows) (default: the trunc rows)
     bool defer_double = false;   // itft's top-level doubling is left to scale() (rows [dbl_lo, dbl_hi): 2^-depth)
     bool fuse_row_last = false;  // the row DIF's last level runs inside the pointwise (k_pwss PAIR)
+    // forward columns: only output rows [own_lo, own_hi) are wanted (own_hi > 0).  After the
+    // first column pass a DIF splits into independent subtrees of positions; the later passes
+    // skip the subtrees outside the rows (MPFFT_SHARD_FWD_COLUMNS_OWN: a rank of the replicated
+    // forward columns keeps only its own rows of each column block)
+    int own_lo = 0, own_hi = 0;
     // forward k_rpass passes hand their pending exponents on to the next pass of the same
     // transform (fwd_columns / fwd_rows).  Every stage still ends exact -- a transform's last
     // level leaves no pending exponent (its pass skips the closing round) -- so the stage API
@@ -678,6 +683,10 @@ struct Exec {
         a.lvl0 = lvl;
         a.rho = (u64)P.w * P.NC;
         a.need = (int)P.Tr;
+        if (own_hi > 0) {   // only rows [own_lo, own_hi) wanted: skip the DIF subtrees outside them
+            a.need = own_hi < a.need ? own_hi : a.need;
+            a.need_lo = own_lo;
+        }
         return a;
     }
 
@@ -1658,6 +1667,10 @@ int mpfft_shard_stage(int stage, const mpfft_shard *sh, const uint64_t *d_i1, co
     case MPFFT_SHARD_FWD_COLUMNS: return X.fwd_columns(d_i1, sh->n1, d_i2, sh->n2, 2);
     case MPFFT_SHARD_FWD_COLUMNS_A: return X.fwd_columns(d_i1, sh->n1, d_i2, sh->n2, 2, 0);
     case MPFFT_SHARD_FWD_COLUMNS_B: return X.fwd_columns(d_i1, sh->n1, d_i2, sh->n2, 2, 1);
+    case MPFFT_SHARD_FWD_COLUMNS_OWN:
+        X.own_lo = sh->r0;
+        X.own_hi = sh->r0 + sh->rcount;
+        return X.fwd_columns(d_i1, sh->n1, d_i2, sh->n2, 2);
     case MPFFT_SHARD_FWD_ROWS: return X.rcount ? X.fwd_rows(2) : MPFFT_OK;
     case MPFFT_SHARD_POINTWISE: return X.pointwise();
     case MPFFT_SHARD_INV_ROWS: return X.rcount ? X.inv_rows() : MPFFT_OK;

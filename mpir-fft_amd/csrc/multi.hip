@@ -493,8 +493,10 @@ int queue_copy(const std::vector<Rank> &rk, const mpfft_copy &c, hipStream_t st)
 }
 
 // replicated forward columns (world 2): rank d runs every column block e's split + column
-// passes from block e's operand slices into its own column arrays (scratch), then plays
-// exchange #1's copies from e to d locally -- its rows of block e into its row layout
+// passes from block e's operand slices into its own column arrays (scratch) -- for its own
+// rows only: after the first pass the passes skip the DIF subtrees that hold none of them
+// (MPFFT_SHARD_FWD_COLUMNS_OWN) -- then plays exchange #1's copies from e to d locally: its
+// rows of block e into its row layout
 int fwd_replicated(const Part &p, std::vector<Rank> &rk, unsigned long depth, unsigned long w)
 {
     std::vector<mpfft_copy> plan;
@@ -507,7 +509,7 @@ int fwd_replicated(const Part &p, std::vector<Rank> &rk, unsigned long depth, un
             mpfft_shard sh = desc(p, d, R, depth, w);
             sh.c0 = (int)(e * p.C);
             const long o = R.whole ? 0 : e * sl;   // block e's slices, or the whole operands
-            int rc = mpfft_shard_stage(MPFFT_SHARD_FWD_COLUMNS, &sh, R.in[0] + o, R.in[1] + o, R.s);
+            int rc = mpfft_shard_stage(MPFFT_SHARD_FWD_COLUMNS_OWN, &sh, R.in[0] + o, R.in[1] + o, R.s);
             if (rc) return rc;
             for (const mpfft_copy &c : plan)
                 if (c.dst == d && c.src == e) {

@@ -703,7 +703,7 @@ __global__ __launch_bounds__(rp_nt(1024 * PP, LOGG, DIR), 4) void k_rpass(PassAr
     const int lo = grp & ((1 << lobits) - 1);
     const int hi = grp >> lobits;
     const int bstart = hi << (a.lbM - a.lvl0);
-    if (DIR == 0 && bstart >= a.need) return;   // whole block past the truncation point (workgroup-uniform)
+    if (DIR == 0 && (bstart >= a.need || bstart + (1 << (a.lbM - a.lvl0)) <= a.need_lo)) return;   // whole block past the truncation point / outside the rows needed (workgroup-uniform)
     BGeo g;
     g.pos0 = bstart | lo;
     g.pstep = 1 << lobits;
@@ -852,7 +852,8 @@ __global__ __launch_bounds__(rp_nt(1024 * PP, LOGG, DIR), 4) void k_rpass(PassAr
     // ---- store (reduced form) --------------------------------------------------------
     if (DIR == 1) rp_pin<G, R>(x);
     rp_store<G, G, PP, NT>(x, st, SLT, [&](int i) -> bool {
-        return DIR == 1 || ((g.pos0 + i * g.pstep) & ~(g.pstep - 1)) < a.need;
+        const int bs = (g.pos0 + i * g.pstep) & ~(g.pstep - 1);
+        return DIR == 1 || (bs < a.need && bs + g.pstep > a.need_lo);
     }, (short *)smem, t);
     if (FILL) {   // IFFT_radix2_truncate's fill (mul_fft.c:1760-1764): b_(p+h) = 2^(p rho) a_p for p >= t - h
         auto fills = [&](int s) -> bool { return g.pos0 + s * g.pstep >= a.fill_lo; };

@@ -95,7 +95,7 @@ __global__ __launch_bounds__(64 * WPB) void k_wpass(PassArgs a)
     const int lo = grp & ((1 << lobits) - 1);
     const int hi = grp >> lobits;
     const int bstart = hi << (a.lbM - a.lvl0);
-    if (DIR == 0 && bstart >= a.need) return;   // whole block past the truncation point
+    if (DIR == 0 && (bstart >= a.need || bstart + (1 << (a.lbM - a.lvl0)) <= a.need_lo)) return;   // whole block past the truncation point / outside the rows needed
     const u64 N2 = 2 * a.N;
     const int pos0 = bstart | lo;
     const int pstep = 1 << lobits;
@@ -183,7 +183,8 @@ __global__ __launch_bounds__(64 * WPB) void k_wpass(PassArgs a)
 
 #pragma unroll
     for (int i = 0; i < G; ++i) {
-        const bool keep = DIR == 1 || ((pos0 + i * pstep) & ~(pstep - 1)) < a.need;
+        const int bs = (pos0 + i * pstep) & ~(pstep - 1);
+        const bool keep = DIR == 1 || (bs < a.need && bs + pstep > a.need_lo);
         if (keep) wv_normalize_store<U, F>(x[i], a.canon != 0, st, slot_of(i), l, lane);
     }
 }

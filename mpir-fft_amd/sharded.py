@@ -256,7 +256,7 @@ class ShardedMul:
             # row layout: exchange #1's copies with every source rank played locally
             recv = [c for c in p.exchange_plan(XCHG_COL_TO_ROW) if c["dst"] == self.rank]
             for d in range(p.world):
-                be.stage("fwd_columns", dict(sh, c0=d * p.C), i1, i2)
+                be.stage("fwd_columns_own", dict(sh, c0=d * p.C), i1, i2)   # this rank's rows of block d
                 for c in recv:
                     if c["src"] == d:
                         f = self._FIELDS[c["field"]]
@@ -439,7 +439,7 @@ class GpuBackend:
 
     def stage(self, name, sh, i1, i2):
         which = {"fwd_columns": 0, "fwd_rows": 1, "pointwise": 2, "inv_rows": 3, "inv_columns": 4,
-                 "fwd_columns_a": 5, "fwd_columns_b": 6}[name]
+                 "fwd_columns_a": 5, "fwd_columns_b": 6, "fwd_columns_own": 7}[name]
         self.mp.shard_stage(which, self._desc(sh), i1, i2, self.stream)
 
     def halo_buffer(self):

@@ -73,7 +73,12 @@ class MockBackend:
     def _fwd_columns_b(self, sh, i1, i2):
         self._fwd_columns(sh, i1, i2, ops=(1,))
 
-    def _fwd_columns(self, sh, i1, i2, ops=(0, 1)):
+    def _fwd_columns_own(self, sh, i1, i2):
+        """only the rank's rows [r0, r0 + rcount) need to be right (MPFFT_SHARD_FWD_COLUMNS_OWN);
+        the other rows are left as garbage, as the GPU stage leaves them unwritten"""
+        self._fwd_columns(sh, i1, i2, rows=range(sh["r0"], sh["r0"] + sh["rcount"]))
+
+    def _fwd_columns(self, sh, i1, i2, ops=(0, 1), rows=None):
         p = self.p
         mask = (1 << p.bits1) - 1
         ch = sh.get("src_chunk", 0)
@@ -89,6 +94,9 @@ class MockBackend:
                 else:
                     xs = [(X >> ((jr * p.NC + c) * p.bits1)) & mask for jr in range(p.Tr)]
                 for pos in range(p.NR):
+                    if rows is not None and pos not in rows:
+                        self.put(sh["col"][k], self.col_slot(sh, pos, cl), 0x5A5A5A5A5A5A5A5A)   # garbage
+                        continue
                     kr = revbin(pos, self.lbR)
                     v = sum(x * self.pw(p.w * p.NC * jr * kr) for jr, x in enumerate(xs) if x)
                     self.put(sh["col"][k], self.col_slot(sh, pos, cl), v)
