@@ -1905,7 +1905,13 @@ int mpfft_release(void)
 // room for the product (make_plan).  Predicted device time = launches x a launch cost +
 // live slots (T) x the measured per-slot cost of a multiply at that coefficient size
 // (CHOOSE_SLOT_NS[log2 l], from scripts/chooser_sweep.py on MI355X:
-// profiles/r02/chooser_sweep.json); the cheapest candidate wins.  Model: a fixed cost
+// profiles/r02/chooser_sweep.json); the cheapest candidate wins.  The round-5 re-sweep
+// (profiles/r05/chooser_sweep.json: l = 2048 196 ns, l = 4096 512 ns per slot, measured at
+// T = 32768 / 16384 slots) is not taken over: a linear per-slot model with those costs picks
+// l = 2048 for 10^6-limb products, whose 2048 live slots fill a quarter of the GPU's
+// pointwise workgroup slots -- the measured per-slot cost does not hold there.  With the r02
+// table the chosen candidate is the fastest of every one timed at all four test sizes
+// (profiles/r05/chooser_check.log, tests/test_gpu_chooser.py at 1.2x).  Model: a fixed cost
 // (launches: ~0.045 ms for the small configurations of the sweep) + T x the marginal
 // per-slot cost at that coefficient size, (ms - 0.045) / T of the sweep.
 static const double CHOOSE_SLOT_NS[13] = {69.7, 26.6, 12.3, 10.4, 7.3, 6.6, 11.0, 13.2, 28.4, 98.2, 167.9, 270.0, 810.7};

@@ -1,12 +1,13 @@
 """GPU check of the (depth, w) chooser (mpfft_choose): at four operand
 sizes the chosen configuration is timed against every other valid candidate whose
 coefficient size is within 4x of the chosen one (device-resident operands, the
-mpfft_mul_device path).  The suite fails only on a gross mis-choice (more than 1.5x the
-fastest): several candidates lie within a few percent of each other, so a tighter bound
+mpfft_mul_device path; the best of 5 timed calls each).  The chosen one must be within 1.2x of
+the fastest: several candidates lie within a few percent of each other, so a tighter bound
 would test the machine's clock state, not the chooser.  The measured ranking is printed
-(profiles/r03/chooser_check.log: the chosen candidate was the fastest at all four sizes).  The reference leaves (depth, w)
+(profiles/r05/chooser_check.log: the chosen candidate was the fastest at all four sizes).  The reference leaves (depth, w)
 to its caller (mul_fft.c:3190-3191); the chooser's cost table comes from
-scripts/chooser_sweep.py (profiles/r02/chooser_sweep.json)."""
+scripts/chooser_sweep.py (profiles/r05/chooser_sweep.json, re-measured against the current
+kernels)."""
 import time
 
 import numpy as np
@@ -62,7 +63,7 @@ def test_chooser_near_best(mp, torch_dev, n):
     assert (d0, w0) in cands
     a = torch.from_numpy(mp.fill_random(n1, 5).view(np.int64)).to(torch_dev)
     b = torch.from_numpy(mp.fill_random(n2, 6).view(np.int64)).to(torch_dev)
-    reps = 5 if n <= 1000000 else 3
+    reps = 5
     times = {c: _time(mp, torch, torch_dev, a, b, n1, n2, c[0], c[1], reps) for c in cands}
     torch.cuda.empty_cache()
     best = min(times.values())
@@ -70,4 +71,4 @@ def test_chooser_near_best(mp, torch_dev, n):
     msg = ", ".join(f"(d={d}, w={wv}, l={mp.plan_info(n1, n2, d, wv)['l']}): {t * 1e3:.3f} ms"
                     for (d, wv), t in ranked[:6])
     print(f"n={n}: chosen (d={d0}, w={w0}, l={l0}) {times[(d0, w0)] * 1e3:.3f} ms; best {msg}")
-    assert times[(d0, w0)] <= 1.5 * best, msg
+    assert times[(d0, w0)] <= 1.2 * best, msg
