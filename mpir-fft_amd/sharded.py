@@ -140,6 +140,7 @@ class ShardedMul:
         # a third row array, which then serves as operand 0's row array (swapped after the stage).
         # At world 1 that array is a view of a third column-layout array, swapped together with
         # col[0], so the row arrays stay views of the column arrays on every run.
+        self._hidx = None   # the halo plan as index tensors (_halo_index)
         self.fused = bool(getattr(backend, "row_fused", lambda: False)())
         self.colc = None
         if self.fused and p.world == 1:
@@ -210,37 +211,55 @@ class ShardedMul:
             plan.append(([v if v is not None else empty for v in send], [v if v is not None else empty for v in recv]))
         return self.comm.exchange(plan, wait=wait)
 
+    def _halo_index(self):
+        """the halo plan as coefficient indices, built once per job: per receiver the column-layout
+        slots this rank sends (in plan order), per sender where its block lands in this rank's
+        halo -- a contiguous range (always when H <= C) or halo slots to scatter to"""
+        if self._hidx is None:
+            import torch
+            p, me, W, l = self.p, self.rank, self.p.world, self.p.l
+            send, runs = [[] for _ in range(W)], [[] for _ in range(W)]
+            for c in p.halo_plan():
+                if c["src"] == me:
+                    send[c["dst"]].extend(range(c["src_off"] // l, (c["src_off"] + c["count"]) // l))
+                if c["dst"] == me:
+                    runs[c["src"]].append((c["dst_off"] // l, c["count"] // l))
+            dev = self.col[0]["dig"].device
+            sidx = [torch.tensor(ix, dtype=torch.int64, device=dev) if ix else None for ix in send]
+            recv = []
+            for d in range(W):
+                r = runs[d]
+                if not r:
+                    recv.append(None)
+                elif all(r[i][0] + r[i][1] == r[i + 1][0] for i in range(len(r) - 1)):
+                    recv.append((r[0][0], sum(n for _, n in r), None))      # straight into the halo
+                else:
+                    ix = [s0 + k for s0, n in r for k in range(n)]
+                    recv.append((0, len(ix), torch.tensor(ix, dtype=torch.int64, device=dev)))
+            self._hidx = (sidx, recv)
+        return self._hidx
+
     def _halo(self, halo):
-        """the H coefficients before each of this rank's stripes into `halo` (Tr H l limbs):
-        one packed message per peer, runs in the library's plan order"""
-        p, me, W = self.p, self.rank, self.p.world
-        src = self.col[0]["dig"]
-        sends, recvs = [[] for _ in range(W)], [[] for _ in range(W)]
-        for c in p.halo_plan():
-            if c["src"] == me:
-                sends[c["dst"]].append(src[c["src_off"]: c["src_off"] + c["count"]])
-            if c["dst"] == me:
-                recvs[c["src"]].append((c["dst_off"], c["count"]))
-        empty = src[:0]
-        send, recv, scatter = [], [], []
-        for d in range(W):
-            send.append(self.be.cat(sends[d]) if sends[d] else empty)
-            runs = recvs[d]
-            n = sum(cnt for _, cnt in runs)
-            if not runs:
+        """the H coefficients before each of this rank's stripes into `halo` (Tr H l limbs): one
+        gathered message per peer (an index_select over the column layout's coefficients)"""
+        p, l = self.p, self.p.l
+        sidx, ridx = self._halo_index()
+        col = self.col[0]["dig"].view(-1, l)
+        empty = self.col[0]["dig"][:0]
+        send = [col.index_select(0, ix).view(-1) if ix is not None else empty for ix in sidx]
+        recv, scatter = [], []
+        for r in ridx:
+            if r is None:
                 recv.append(empty)
-            elif all(runs[i][0] + runs[i][1] == runs[i + 1][0] for i in range(len(runs) - 1)):
-                recv.append(halo[runs[0][0]: runs[0][0] + n])      # dst-contiguous: straight in
+            elif r[2] is None:
+                recv.append(halo[r[0] * l: (r[0] + r[1]) * l])
             else:
-                buf = halo.new_empty(n)
+                buf = halo.new_empty(r[1] * l)
                 recv.append(buf)
-                scatter.append((buf, runs))
+                scatter.append((buf, r[2]))
         self.comm.exchange([(send, recv)], wait=True)
-        for buf, runs in scatter:
-            o = 0
-            for off, cnt in runs:
-                halo[off: off + cnt].copy_(buf[o: o + cnt])
-                o += cnt
+        for buf, ix in scatter:
+            halo.view(-1, l).index_copy_(0, ix, buf.view(-1, l))
 
     def run(self, i1, i2, mark=None):
         """i1, i2: this rank's operand column slices (ShardPlan.slice_operand; the full
@@ -447,9 +466,6 @@ class GpuBackend:
         if getattr(self, "_halo_t", None) is None:
             self._halo_t = self.torch.zeros(p.Tr * p.H * p.l, dtype=self.torch.int64, device=self.dev)
         return self._halo_t
-
-    def cat(self, views):
-        return self.torch.cat(views)
 
     def combine(self, sh, phase, halo, sums_all=None):
         """phase 0: (stripes, summaries) with carry-in 0; phase 1: each stripe's carry-in from

@@ -211,10 +211,6 @@ class MockBackend:
         p = self.p
         return torch.zeros(p.Tr * p.H * p.l, dtype=torch.int64)
 
-    @staticmethod
-    def cat(views):
-        return torch.cat(views)
-
     def _coef(self, sh, j, kbase, k, halo):
         p = self.p
         if k < kbase:
