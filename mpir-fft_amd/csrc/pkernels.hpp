@@ -122,7 +122,10 @@ __host__ __device__ __forceinline__ int pw_norm(u64 (&L)[M], int T)
 // After pw_norm T_q = -1, so the (1 + T_q) term is a rare branch, and the whole sum is
 // one add-with-carry chain with carry-in 1.
 // packed: the partner's 2 T_q + S_q (TT[q], or a register in the tight form)
-template <int M, int LK, int PD = 2 * M>
+// FIXE >= 0: the caller guarantees E mod N' == FIXE, so the rotation is a compile-time constant
+// and every wrap test, word address and complement mask below folds away (the forward
+// transforms' first level, where E is exactly N'/2 for every thread: pw_transform)
+template <int M, int LK, int PD = 2 * M, int FIXE = -1>
 __host__ __device__ __forceinline__ void pw_combine(u64 (&L)[M], int &T, int &S, int alpha, const u32 *Xw,
                                                    int packed, int q, unsigned E)
 {
@@ -131,6 +134,7 @@ __host__ __device__ __forceinline__ void pw_combine(u64 (&L)[M], int &T, int &S,
     const int Tq = packed >> 1, Sq = packed & 1;
     bool neg = E >= NP;
     if (neg) E -= NP;
+    if (FIXE >= 0) E = (unsigned)FIXE;
     const int Yw = ((int)E - 1) >> 5;                    // E = 0: Yw = -1, s5 = 32
     const unsigned sh = (unsigned)(32 * (Yw + 1)) - E;   // 32 - s5, in [0, 31]
     if (alpha == 0) {
@@ -402,63 +406,78 @@ __device__ __forceinline__ void pw_wave_sync()
     asm volatile("" ::: "memory");
 }
 
+// one level jj of the transform; FIX0: the forward transform's first level, whose rotation is the
+// compile-time N'/2 (pw_combine FIXE)
+template <int M, int LK, int DIR, bool FIX0>
+__device__ __forceinline__ void pw_level(u64 (&L)[M], int &T, int &S, unsigned &P, u32 *Xw, int *TT, unsigned *PP,
+                                         unsigned W2, int t, int jj)
+{
+    constexpr int K = 1 << LK, lk = LK;
+    constexpr unsigned N2 = 128 * M;
+    const int j = DIR == 0 ? jj : lk - 1 - jj;   // DIF level index (DIT runs them backwards)
+    const int h = K >> (j + 1);
+    const int q = t ^ h;
+    const bool top = !(t & h);
+    const int qt = t & ~h;                       // top index of the pair
+    // (qt mod h) 2^j < K/2, times W2: below N' (= K W2 / 2): no reduction needed
+    const unsigned tw = (unsigned)((qt & (h - 1)) << j) * W2;
+    const bool cross = h >= 64;                  // partner in another wave
+    unsigned Pq;
+    int packed;
+    if (pw_tight(K)) {
+        // the partner's top / sign and exponent first (a shuffle, or through rows 0-1 before
+        // the words overwrite them), then the words
+        T = pw_norm<M>(L, T);
+        const int own = 2 * T + S;
+        if (cross) {
+            Xw[t] = (u32)own;
+            Xw[K + t] = P;
+            __syncthreads();
+            packed = (int)Xw[q];
+            Pq = Xw[K + q];
+            __syncthreads();
+        } else {
+            packed = __shfl_xor(own, h);
+            Pq = (unsigned)__shfl_xor((int)P, h);
+        }
+        pw_publish_words<M, LK>(L, Xw, t);
+        if (cross) __syncthreads(); else pw_wave_sync();
+    } else {
+        pw_publish<M, LK>(L, T, S, Xw, TT, t);
+        PP[t] = P;
+        if (cross) __syncthreads(); else pw_wave_sync();
+        Pq = PP[q];
+        packed = TT[q];
+    }
+    unsigned E;
+    if (DIR == 0) {
+        // top: X_t + X_q = 2^P (x_t + 2^(Pq-P) x_q); bottom: (X_q - X_t) w^tw = 2^(P+tw) (2^(Pq-P) x_q - x_t)
+        E = pw_mod(Pq + N2 - P, N2);
+        pw_combine<M, LK, pw_pd<M, LK>(), FIX0 ? 32 * M : -1>(L, T, S, top ? 1 : -1, Xw, packed, q, E);
+        if (!top) P = pw_mod(P + tw, N2);
+    } else {
+        // top: Z_t + Z_q w^-tw = 2^P (z_t + 2^(Pq-tw-P) z_q)
+        // bottom: Z_q - Z_t w^-tw = 2^(P-tw) (2^(Pq-P+tw) z_q - z_t)
+        E = top ? pw_mod(Pq + 2 * N2 - tw - P, N2) : pw_mod(Pq + N2 - P + tw, N2);
+        pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, top ? 1 : -1, Xw, packed, q, E);
+        if (!top) P = pw_mod(P + N2 - tw, N2);
+    }
+    if (cross) __syncthreads(); else pw_wave_sync();
+}
+
 template <int M, int LK, int DIR>
 __device__ __forceinline__ void pw_transform(u64 (&L)[M], int &T, int &S, unsigned &P, u32 *Xw, int *TT, unsigned *PP,
                                              unsigned W2, int t)
 {
-    constexpr int K = 1 << LK, lk = LK;
-    constexpr unsigned N2 = 128 * M;
-    for (int jj = 0; jj < lk; ++jj) {
-        const int j = DIR == 0 ? jj : lk - 1 - jj;   // DIF level index (DIT runs them backwards)
-        const int h = K >> (j + 1);
-        const int q = t ^ h;
-        const bool top = !(t & h);
-        const int qt = t & ~h;                       // top index of the pair
-        // (qt mod h) 2^j < K/2, times W2: below N' (= K W2 / 2): no reduction needed
-        const unsigned tw = (unsigned)((qt & (h - 1)) << j) * W2;
-        const bool cross = h >= 64;                  // partner in another wave
-        unsigned Pq;
-        int packed;
-        if (pw_tight(K)) {
-            // the partner's top / sign and exponent first (a shuffle, or through rows 0-1 before
-            // the words overwrite them), then the words
-            T = pw_norm<M>(L, T);
-            const int own = 2 * T + S;
-            if (cross) {
-                Xw[t] = (u32)own;
-                Xw[K + t] = P;
-                __syncthreads();
-                packed = (int)Xw[q];
-                Pq = Xw[K + q];
-                __syncthreads();
-            } else {
-                packed = __shfl_xor(own, h);
-                Pq = (unsigned)__shfl_xor((int)P, h);
-            }
-            pw_publish_words<M, LK>(L, Xw, t);
-            if (cross) __syncthreads(); else pw_wave_sync();
-        } else {
-            pw_publish<M, LK>(L, T, S, Xw, TT, t);
-            PP[t] = P;
-            if (cross) __syncthreads(); else pw_wave_sync();
-            Pq = PP[q];
-            packed = TT[q];
-        }
-        unsigned E;
-        if (DIR == 0) {
-            // top: X_t + X_q = 2^P (x_t + 2^(Pq-P) x_q); bottom: (X_q - X_t) w^tw = 2^(P+tw) (2^(Pq-P) x_q - x_t)
-            E = pw_mod(Pq + N2 - P, N2);
-            pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, top ? 1 : -1, Xw, packed, q, E);
-            if (!top) P = pw_mod(P + tw, N2);
-        } else {
-            // top: Z_t + Z_q w^-tw = 2^P (z_t + 2^(Pq-tw-P) z_q)
-            // bottom: Z_q - Z_t w^-tw = 2^(P-tw) (2^(Pq-P+tw) z_q - z_t)
-            E = top ? pw_mod(Pq + 2 * N2 - tw - P, N2) : pw_mod(Pq + N2 - P + tw, N2);
-            pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, top ? 1 : -1, Xw, packed, q, E);
-            if (!top) P = pw_mod(P + N2 - tw, N2);
-        }
-        if (cross) __syncthreads(); else pw_wave_sync();
+    int jj = 0;
+    if (DIR == 0) {
+        // first level: every P is still its negacyclic weight floor(t W2 / 2) (+ N'/4 for a half
+        // exponent, equal for t and q = t ^ K/2), so Pq - P = +-(K/2) W2 / 2 = +-N'/2: E mod N'
+        // is N'/2 for every thread -- a rotation by exactly M words, peeled off the loop
+        pw_level<M, LK, DIR, true>(L, T, S, P, Xw, TT, PP, W2, t, 0);
+        jj = 1;
     }
+    for (; jj < LK; ++jj) pw_level<M, LK, DIR, false>(L, T, S, P, Xw, TT, PP, W2, t, jj);
 }
 
 // Piece t of a coefficient in the reduced HBM form (coeff.hpp: limbs + carry masks +
