@@ -406,9 +406,29 @@ __device__ __forceinline__ void pw_wave_sync()
     asm volatile("" ::: "memory");
 }
 
-// one level jj of the transform; FIX0: the forward transform's first level, whose rotation is the
-// compile-time N'/2 (pw_combine FIXE)
-template <int M, int LK, int DIR, bool FIX0>
+// the combine of a forward level j whose rotation E mod N' is one of the odd multiples of
+// N' / 2^(j+1) and the same for the whole wave: a scalar switch to the compile-time rotation
+// (pw_combine FIXE); anything else (never, by pw_transform's derivation) takes the general form
+template <int M, int LK, int J, int I = 0>
+__device__ __forceinline__ void pw_combine_fixed(u64 (&L)[M], int &T, int &S, int alpha, const u32 *Xw, int packed, int q,
+                                                 unsigned E, unsigned Eu)
+{
+    constexpr unsigned NP = 64 * M;
+    if constexpr (I < (1 << J)) {
+        constexpr unsigned C = (2 * I + 1) * (NP >> (J + 1));
+        if (Eu == C) {
+            pw_combine<M, LK, pw_pd<M, LK>(), (int)C>(L, T, S, alpha, Xw, packed, q, E);
+            return;
+        }
+        pw_combine_fixed<M, LK, J, I + 1>(L, T, S, alpha, Xw, packed, q, E, Eu);
+    } else {
+        pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, alpha, Xw, packed, q, E);
+    }
+}
+
+// one level jj of the transform.  FIXJ >= 0 (forward transforms, level jj = FIXJ): E mod N' is
+// wave-uniform and one of 2^FIXJ compile-time values (level 0: exactly N'/2) -- pw_transform
+template <int M, int LK, int DIR, int FIXJ>
 __device__ __forceinline__ void pw_level(u64 (&L)[M], int &T, int &S, unsigned &P, u32 *Xw, int *TT, unsigned *PP,
                                          unsigned W2, int t, int jj)
 {
@@ -453,7 +473,19 @@ __device__ __forceinline__ void pw_level(u64 (&L)[M], int &T, int &S, unsigned &
     if (DIR == 0) {
         // top: X_t + X_q = 2^P (x_t + 2^(Pq-P) x_q); bottom: (X_q - X_t) w^tw = 2^(P+tw) (2^(Pq-P) x_q - x_t)
         E = pw_mod(Pq + N2 - P, N2);
-        pw_combine<M, LK, pw_pd<M, LK>(), FIX0 ? 32 * M : -1>(L, T, S, top ? 1 : -1, Xw, packed, q, E);
+        if constexpr (FIXJ == 0) {
+            pw_combine<M, LK, pw_pd<M, LK>(), 32 * M>(L, T, S, top ? 1 : -1, Xw, packed, q, E);
+        } else if constexpr (FIXJ > 0) {
+            constexpr unsigned NP = 64 * M;
+            const unsigned Em = E >= NP ? E - NP : E;
+            const unsigned Eu = (unsigned)__builtin_amdgcn_readfirstlane((int)Em);
+            if (__all(Em == Eu))   // (wave-uniform by construction; checked, as the fixed forms rely on it)
+                pw_combine_fixed<M, LK, FIXJ>(L, T, S, top ? 1 : -1, Xw, packed, q, E, Eu);
+            else
+                pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, top ? 1 : -1, Xw, packed, q, E);
+        } else {
+            pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, top ? 1 : -1, Xw, packed, q, E);
+        }
         if (!top) P = pw_mod(P + tw, N2);
     } else {
         // top: Z_t + Z_q w^-tw = 2^P (z_t + 2^(Pq-tw-P) z_q)
@@ -471,13 +503,24 @@ __device__ __forceinline__ void pw_transform(u64 (&L)[M], int &T, int &S, unsign
 {
     int jj = 0;
     if (DIR == 0) {
-        // first level: every P is still its negacyclic weight floor(t W2 / 2) (+ N'/4 for a half
-        // exponent, equal for t and q = t ^ K/2), so Pq - P = +-(K/2) W2 / 2 = +-N'/2: E mod N'
-        // is N'/2 for every thread -- a rotation by exactly M words, peeled off the loop
-        pw_level<M, LK, DIR, true>(L, T, S, P, Xw, TT, PP, W2, t, 0);
-        jj = 1;
+        // The forward levels' rotations at the top of the DIF.  Before level j, P_t is the weight
+        // floor(t W2 / 2) (+ N'/4 for a half exponent: equal for t and its partner q = t ^ h_j) plus,
+        // for every earlier level j' whose bit h_j' = K >> (j'+1) t has, the twiddle
+        // ((t mod h_j') << j') W2.  q differs from t in bit h_j only, so
+        //   E = Pq - P = +-[h_j W2 / 2 + sum_(j' < j, bit h_j' of t) (h_j << j') W2]
+        //     = +-[N' / 2^(j+1) + sum N' / 2^(j - j')]   (K W2 = 2 N'),
+        // an odd multiple of N' / 2^(j+1), fixed by the bits h_0 .. h_(j-1) of t and the sign by
+        // bit h_j: wave-uniform while h_j >= 64.  Level 0: exactly N'/2 for every thread; levels
+        // 1 .. log2(K/128): one of 2^j values, a scalar switch to the compile-time rotation (the
+        // per-word wrap tests, addresses and complement masks fold away).  Each level is its own
+        // inlined copy (peeled off the loop: one loop body with both forms spilled 3x more).
+        static_assert(LK >= 7, "level 0's partner K/2 >= 64 lanes away");
+        pw_level<M, LK, DIR, 0>(L, T, S, P, Xw, TT, PP, W2, t, 0);
+        if constexpr (LK >= 8) pw_level<M, LK, DIR, 1>(L, T, S, P, Xw, TT, PP, W2, t, 1);   // h = K/4 >= 64
+        if constexpr (LK >= 9) pw_level<M, LK, DIR, 2>(L, T, S, P, Xw, TT, PP, W2, t, 2);   // h = K/8 >= 64
+        jj = LK >= 9 ? 3 : LK >= 8 ? 2 : 1;
     }
-    for (; jj < LK; ++jj) pw_level<M, LK, DIR, false>(L, T, S, P, Xw, TT, PP, W2, t, jj);
+    for (; jj < LK; ++jj) pw_level<M, LK, DIR, -1>(L, T, S, P, Xw, TT, PP, W2, t, jj);
 }
 
 // Piece t of a coefficient in the reduced HBM form (coeff.hpp: limbs + carry masks +
