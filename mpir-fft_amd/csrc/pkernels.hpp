@@ -409,20 +409,23 @@ __device__ __forceinline__ void pw_wave_sync()
 // the combine of a forward level j whose rotation E mod N' is one of the odd multiples of
 // N' / 2^(j+1) and the same for the whole wave: a scalar switch to the compile-time rotation
 // (pw_combine FIXE); anything else (never, by pw_transform's derivation) takes the general form
+// (Eu = the wave's E mod N', an odd multiple (2I + 1) N' / 2^(J+1): I selects the copy; the last
+// copy also takes any other value, which pw_transform's derivation rules out -- checked exactly
+// for both kernel shapes by tests/test_pw_host.py's simulation of the pending exponents)
 template <int M, int LK, int J, int I = 0>
 __device__ __forceinline__ void pw_combine_fixed(u64 (&L)[M], int &T, int &S, int alpha, const u32 *Xw, int packed, int q,
                                                  unsigned E, unsigned Eu)
 {
     constexpr unsigned NP = 64 * M;
-    if constexpr (I < (1 << J)) {
-        constexpr unsigned C = (2 * I + 1) * (NP >> (J + 1));
+    constexpr unsigned C = (2 * I + 1) * (NP >> (J + 1));
+    if constexpr (I + 1 < (1 << J)) {
         if (Eu == C) {
             pw_combine<M, LK, pw_pd<M, LK>(), (int)C>(L, T, S, alpha, Xw, packed, q, E);
             return;
         }
         pw_combine_fixed<M, LK, J, I + 1>(L, T, S, alpha, Xw, packed, q, E, Eu);
     } else {
-        pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, alpha, Xw, packed, q, E);
+        pw_combine<M, LK, pw_pd<M, LK>(), (int)C>(L, T, S, alpha, Xw, packed, q, E);
     }
 }
 
@@ -478,11 +481,8 @@ __device__ __forceinline__ void pw_level(u64 (&L)[M], int &T, int &S, unsigned &
         } else if constexpr (FIXJ > 0) {
             constexpr unsigned NP = 64 * M;
             const unsigned Em = E >= NP ? E - NP : E;
-            const unsigned Eu = (unsigned)__builtin_amdgcn_readfirstlane((int)Em);
-            if (__all(Em == Eu))   // (wave-uniform by construction; checked, as the fixed forms rely on it)
-                pw_combine_fixed<M, LK, FIXJ>(L, T, S, top ? 1 : -1, Xw, packed, q, E, Eu);
-            else
-                pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, top ? 1 : -1, Xw, packed, q, E);
+            const unsigned Eu = (unsigned)__builtin_amdgcn_readfirstlane((int)Em);   // wave-uniform (above)
+            pw_combine_fixed<M, LK, FIXJ>(L, T, S, top ? 1 : -1, Xw, packed, q, E, Eu);
         } else {
             pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, top ? 1 : -1, Xw, packed, q, E);
         }
