@@ -101,6 +101,130 @@ __device__ __forceinline__ void comb_limb(const CombArgs &a, const StripeView &s
 }
 
 // --------------------------------------------------------------------------
+// Consecutive limbs per thread (k_combine1<8, KM, true>): thread t sums the windows of limbs
+// mA .. mA + 7 (mA = base + 8 t).  The coefficients covering the wave's 512 limbs are found
+// once per wave (KM of them at most, host), and every one of them is one word offset and one
+// bit shift for all eight limbs: each lane loads the 10 words around its window as five
+// aligned 16-B pairs (out-of-range pairs read as zero: before the coefficient, past its l
+// words, or a coefficient that does not reach the lane's limbs) and forms each limb with two
+// funnel shifts.  Bit b_i = 64 (m0 + mA + i) - k bits1 of c_k is dword 2i + D, shift sh, of the
+// loaded pairs (D, sh uniform per coefficient: the lanes' limbs differ by multiples of 8).
+// --------------------------------------------------------------------------
+typedef u64 cb_v2u __attribute__((ext_vector_type(2)));
+
+template <int D>
+__device__ __forceinline__ void comb_acc8(const u32 (&W)[20], int sh, u64 (&lo)[8], u32 (&hi)[8])
+{
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const u32 x0 = W[2 * i + D], x1 = W[2 * i + D + 1], x2 = W[2 * i + D + 2];
+        const u64 v = ((u64)__builtin_amdgcn_alignbit(x2, x1, sh) << 32) | __builtin_amdgcn_alignbit(x1, x0, sh);
+        u64 s;
+        hi[i] += add_ovf(lo[i], v, &s);
+        lo[i] = s;
+    }
+}
+
+// mW: the wave's first limb (stripe-relative), mA this lane's; total: the stripe's limbs.
+// XP: the wave's 257 pairs of a coefficient are loaded coalesced (lane L: pairs L + 64 p) and
+// handed to their lanes through the wave's LDS region X (257 x 16 B)
+template <int KM, bool XP = false>
+__device__ __forceinline__ void comb_thread8(const CombArgs &a, const StripeView &sv, long m0, long mW, long mA,
+                                             long total, u64 (&lo)[8], u32 (&hi)[8], cb_v2u *X = nullptr)
+{
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        lo[i] = 0;
+        hi[i] = 0;
+    }
+    if (mW >= total) return;
+    const long wl = mW + 512 < total ? mW + 512 : total;
+    const u64 P = (u64)(m0 + mW) * 64, Pl = (u64)(m0 + wl - 1) * 64;
+    const long klo = (P >= a.N) ? udiv_inv(P - a.N, a.bits1, a.inv_bits1) + 1 : 0;
+    long khi = udiv_inv(Pl + 63, a.bits1, a.inv_bits1);
+    if (khi > a.len - 1) khi = a.len - 1;
+    const long lp = a.l / 2;
+    u32 W[KM][20];
+    int S2[KM];
+#pragma unroll
+    for (int j = 0; j < KM; ++j) {   // every coefficient's pairs requested before any is used
+        const long k = klo + j;
+        const bool in = k <= khi;
+        const i64 o = (i64)(64 * (u64)(m0 + mA) + 64) - (i64)((u64)k * a.bits1);
+        const long q = (long)(o >> 6) - 1;   // word of c_k holding limb mA's bit 0 (arithmetic)
+        S2[j] = (int)(o & 63) + 64 * (int)(q & 1);
+        const long pb = q >> 1;
+        const long d = k - sv.kbase;
+        const u64 *cp = d < 0 ? sv.chalo + (d + a.H) * (long)a.l : sv.cdig + d * (long)a.l;
+        if constexpr (XP) {
+            const int L = (int)(mA - mW) >> 3;
+            const long pw = pb - 4 * L;   // the wave's first pair
+#pragma unroll
+            for (int p = 0; p < 5; ++p) {
+                const long pp = pw + L + 64 * p;
+                cb_v2u x = {0, 0};
+                if (in && (p < 4 || L == 0) && pp >= 0 && pp < lp) x = *(const cb_v2u *)(cp + 2 * pp);
+                W[j][4 * p] = (u32)x.x;
+                W[j][4 * p + 1] = (u32)(x.x >> 32);
+                W[j][4 * p + 2] = (u32)x.y;
+                W[j][4 * p + 3] = (u32)(x.y >> 32);
+            }
+        } else {
+#pragma unroll
+            for (int p = 0; p < 5; ++p) {
+                const long pp = pb + p;
+                cb_v2u x = {0, 0};
+                if (in && pp >= 0 && pp < lp) x = *(const cb_v2u *)(cp + 2 * pp);
+                W[j][4 * p] = (u32)x.x;
+                W[j][4 * p + 1] = (u32)(x.x >> 32);
+                W[j][4 * p + 2] = (u32)x.y;
+                W[j][4 * p + 3] = (u32)(x.y >> 32);
+            }
+        }
+    }
+    if constexpr (XP) {   // lane L's pairs 4L .. 4L + 4 of the wave's 257
+        const int L = (int)(mA - mW) >> 3;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+#pragma unroll
+            for (int p = 0; p < 5; ++p)
+                if (p < 4 || L == 0) {
+                    cb_v2u x;
+                    x.x = ((u64)W[j][4 * p + 1] << 32) | W[j][4 * p];
+                    x.y = ((u64)W[j][4 * p + 3] << 32) | W[j][4 * p + 2];
+                    X[L + 64 * p] = x;
+                }
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int p = 0; p < 5; ++p) {
+                const cb_v2u x = X[4 * L + p];
+                W[j][4 * p] = (u32)x.x;
+                W[j][4 * p + 1] = (u32)(x.x >> 32);
+                W[j][4 * p + 2] = (u32)x.y;
+                W[j][4 * p + 3] = (u32)(x.y >> 32);
+            }
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < KM; ++j) {
+        if (klo + j > khi) break;
+        const int s2 = __builtin_amdgcn_readfirstlane(S2[j]);
+        const int sh = s2 & 31;
+        switch (s2 >> 5) {
+        case 0: comb_acc8<0>(W[j], sh, lo, hi); break;
+        case 1: comb_acc8<1>(W[j], sh, lo, hi); break;
+        case 2: comb_acc8<2>(W[j], sh, lo, hi); break;
+        default: comb_acc8<3>(W[j], sh, lo, hi); break;
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
 // k_combine1<V, KM>: nst stripes in one launch, bps blocks of 256 V limbs each.  Block
 // (j, b) owns limbs [256 V b, 256 V (b+1)) of stripe j: it sums their coefficient windows
 // (coalesced, limb base + k 256 + t), resolves its carries locally, and gets its carry-in by
@@ -116,12 +240,14 @@ __device__ __forceinline__ void comb_limb(const CombArgs &a, const StripeView &s
 // overflow of its last limb's window sum belongs to the next stripe (its limb ms - 1).
 // allp_out (or null): per block, 1 if all its limbs propagate (k_comb_summary).
 // --------------------------------------------------------------------------
-template <int CB_V, int KM>
-__global__ __launch_bounds__(256) void k_combine1(CombArgs a, u64 *r, u32 *st, u32 *allp_out)
+template <int CB_V, int KM, bool CT = false, int NT = 256, bool XP = false>
+__global__ __launch_bounds__(NT) void k_combine1(CombArgs a, u64 *r, u32 *st, u32 *allp_out)
 {
-    constexpr int CB_LIMBS = 256 * CB_V;
+    constexpr int CB_LIMBS = NT * CB_V;
+    static_assert(!CT || (CB_V == 8 && KM > 0), "consecutive limbs per thread: V = 8, a fixed coefficient count");
+    static_assert(CT || NT == 256, "the per-limb form runs 256 threads");
     __shared__ u64 L[CB_LIMBS];
-    __shared__ u32 H[CB_LIMBS + 1];
+    __shared__ u32 H[CT ? NT + 1 : CB_LIMBS + 1];
     __shared__ u64 scr[64];
     __shared__ u32 sh_cin, sh_b;
     const WG c = wg_ctx();
@@ -137,38 +263,68 @@ __global__ __launch_bounds__(256) void k_combine1(CombArgs a, u64 *r, u32 *st, u
     sv.cdig = a.dig + j * a.C * (long)a.l;
     sv.chalo = a.halo ? a.halo + j * (long)a.H * a.l : nullptr;
     const long base = b * CB_LIMBS;
-    // window sums: lo of limb base + i -> L[i], its carry (hi) -> H[i + 1]
-#pragma unroll
-    for (int k = 0; k < CB_V; ++k) {
-        const int i = k * 256 + c.t;
-        const long m = base + i;
-        u64 lo = 0;
-        u32 hi = 0;
-        if (m < total) comb_limb<KM>(a, sv, m0 + m, &lo, &hi);
-        L[i] = lo;
-        H[i + 1] = hi;
-    }
-    if (c.t == 0) {
-        u64 lo = 0;
-        u32 hi = 0;
-        if (m0 + base > 0 && base < total) comb_limb<KM>(a, sv, m0 + base - 1, &lo, &hi);
-        H[0] = hi;
-    }
-    __syncthreads();
-    // thread t: limbs base + t V .. + V - 1, value v = L + H (H carries the limb below's overflow)
+    // thread t: limbs base + t V .. + V - 1, value v = window sum + the limb below's overflow
     u64 v[CB_V];
     u32 g = 0, p = 0;
     bool G = false, Pa = true;
+    if constexpr (CT) {
+        u64 lo[8];
+        u32 hi[8];
+        const int t0 = __builtin_amdgcn_readfirstlane(c.t & ~63);
+        if constexpr (XP) {
+            __shared__ cb_v2u XS[NT / 64][257];
+            comb_thread8<KM, true>(a, sv, m0, base + 8L * t0, base + 8L * c.t, total, lo, hi, XS[c.wave]);
+        } else {
+            comb_thread8<KM>(a, sv, m0, base + 8L * t0, base + 8L * c.t, total, lo, hi);
+        }
+        H[c.t + 1] = hi[7];
+        if (c.t == 0) {
+            u64 l0 = 0;
+            u32 h0 = 0;
+            if (m0 + base > 0 && base < total) comb_limb<KM>(a, sv, m0 + base - 1, &l0, &h0);   // KM >= a limb's count
+            H[0] = h0;
+        }
+        __syncthreads();
 #pragma unroll
-    for (int k = 0; k < CB_V; ++k) {
-        const int i = c.t * CB_V + k;
-        const bool real = base + i < total;
-        const bool gk = add_ovf(L[i], (u64)H[i], &v[k]) && real;
-        const bool pk = v[k] == MPF_MAXL || !real;
-        g |= (u32)gk << k;
-        p |= (u32)pk << k;
-        G = gk || (pk && G);
-        Pa = Pa && pk;
+        for (int k = 0; k < CB_V; ++k) {
+            const bool real = base + c.t * CB_V + k < total;
+            const bool gk = add_ovf(lo[k], (u64)(k ? hi[k - 1] : H[c.t]), &v[k]) && real;
+            const bool pk = v[k] == MPF_MAXL || !real;
+            g |= (u32)gk << k;
+            p |= (u32)pk << k;
+            G = gk || (pk && G);
+            Pa = Pa && pk;
+        }
+    } else {
+        // window sums: lo of limb base + i -> L[i], its carry (hi) -> H[i + 1]
+#pragma unroll
+        for (int k = 0; k < CB_V; ++k) {
+            const int i = k * 256 + c.t;
+            const long m = base + i;
+            u64 lo = 0;
+            u32 hi = 0;
+            if (m < total) comb_limb<KM>(a, sv, m0 + m, &lo, &hi);
+            L[i] = lo;
+            H[i + 1] = hi;
+        }
+        if (c.t == 0) {
+            u64 lo = 0;
+            u32 hi = 0;
+            if (m0 + base > 0 && base < total) comb_limb<KM>(a, sv, m0 + base - 1, &lo, &hi);
+            H[0] = hi;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < CB_V; ++k) {
+            const int i = c.t * CB_V + k;
+            const bool real = base + i < total;
+            const bool gk = add_ovf(L[i], (u64)H[i], &v[k]) && real;
+            const bool pk = v[k] == MPF_MAXL || !real;
+            g |= (u32)gk << k;
+            p |= (u32)pk << k;
+            G = gk || (pk && G);
+            Pa = Pa && pk;
+        }
     }
     u32 co0;
     wg_scan<1>(c, G, Pa, 0, &co0, scr);
@@ -209,8 +365,8 @@ __global__ __launch_bounds__(256) void k_combine1(CombArgs a, u64 *r, u32 *st, u
     u64 *rs = r + j * a.SL;
 #pragma unroll
     for (int k = 0; k < CB_V; ++k) {
-        const long m = base + k * 256 + c.t;
-        if (m < total) rs[m] = L[k * 256 + c.t];
+        const long m = base + k * NT + c.t;
+        if (m < total) rs[m] = L[k * NT + c.t];
     }
 }
 

@@ -406,9 +406,28 @@ struct Exec {
                                   return x == 1 || x == 2 || x == 4 || x == 16 ? x : 8; }();
         return v;
     }
-    static long comb_blocks(long mcount) { return (mcount + 256L * comb_v() - 1) / (256L * comb_v()); }
+    // k_combine1's form for plan P: consecutive limbs per thread (combine.hpp) where a wave's 512
+    // limbs meet at most 4 coefficients, else the per-limb form (MPFFT_COMB_CT = 0: per-limb, A/B)
+    static int comb_kw(const Plan &P) { return (int)((P.N + 32767) / P.bits1 + 1); }
+    static bool comb_ct(const Plan &P)
+    {
+        static const bool no_ct = [] { const char *e = diag_env("MPFFT_COMB_CT"); return e && !strcmp(e, "0"); }();
+        return comb_v() == 8 && !no_ct && comb_kw(P) <= 4;
+    }
+    // threads per k_combine1 block: 512 for the consecutive form (C3 combine 0.285 -> 0.266 ms
+    // against 256, profiles/r05/combine_ct_ab.txt; MPFFT_COMB_NT = 256 for A/B), 256 per-limb
+    static int comb_nt(const Plan &P)
+    {
+        static const int nt = [] { const char *e = diag_env("MPFFT_COMB_NT"); return e && atoi(e) == 256 ? 256 : 512; }();
+        return comb_ct(P) ? nt : 256;
+    }
+    static long comb_blocks(const Plan &P, long mcount)
+    {
+        const long bl = (long)comb_nt(P) * comb_v();
+        return (mcount + bl - 1) / bl;
+    }
     u32 *comb_flags(unsigned char *ws) const { return (u32 *)(ws + P.off_flags); }
-    static long comb_flag_words(long mcount) { return (comb_blocks(mcount) + 4) / 4 * 4; }
+    static long comb_flag_words(const Plan &P, long mcount) { return (comb_blocks(P, mcount) + 4) / 4 * 4; }
 
     // single-GPU workspace: both layouts are the natural one
     void single(unsigned char *ws)
@@ -1192,7 +1211,7 @@ struct Exec {
         a.len = P.len;
         a.total = P.total;
         a.inv_bits1 = 1.0 / (double)P.bits1;
-        a.bps = comb_blocks(stripe_limbs);
+        a.bps = comb_blocks(P, stripe_limbs);
         const long nb = nst * a.bps;
         if (!cleared) HIPCHK(hipMemsetAsync(st, 0, (size_t)(nb + 1) * 4, s));   // one fill
         const int v = comb_v();
@@ -1202,7 +1221,18 @@ struct Exec {
                   : v == 16 ? k_combine1<16, 3> : k_combine1<8, 3>)
                : (v == 1 ? k_combine1<1, 0> : v == 2 ? k_combine1<2, 0> : v == 4 ? k_combine1<4, 0>
                   : v == 16 ? k_combine1<16, 0> : k_combine1<8, 0>);
-        hipLaunchKernelGGL(f, dim3((unsigned)nb), dim3(256), 0, s, a, r, st, allp);   // st[nb]: the ticket counter
+        // consecutive limbs per thread: the wave's pairs loaded coalesced and handed out through LDS
+        // (C3 combine 0.300 -> 0.285 ms against per-lane pair loads; MPFFT_COMB_XP = 0 for A/B)
+        static const bool no_xp = [] { const char *e = diag_env("MPFFT_COMB_XP"); return e && !strcmp(e, "0"); }();
+        const int nt = comb_nt(P);
+        if (comb_ct(P)) {
+            const bool k3w = comb_kw(P) <= 3;
+            if (!no_xp) f = nt == 512 ? (k3w ? k_combine1<8, 3, true, 512, true> : k_combine1<8, 4, true, 512, true>)
+                                      : (k3w ? k_combine1<8, 3, true, 256, true> : k_combine1<8, 4, true, 256, true>);
+            else f = nt == 512 ? (k3w ? k_combine1<8, 3, true, 512> : k_combine1<8, 4, true, 512>)
+                               : (k3w ? k_combine1<8, 3, true> : k_combine1<8, 4, true>);
+        }
+        hipLaunchKernelGGL(f, dim3((unsigned)nb), dim3(nt), 0, s, a, r, st, allp);   // st[nb]: the ticket counter
         HIPCHK(hipGetLastError());
         return MPFFT_OK;
     }
@@ -1372,7 +1402,7 @@ static int run_all(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, un
     Exec X(P, s);
     X.single(ws);
     X.zflags = X.comb_flags(ws);
-    X.zflags_n = X.comb_flag_words(P.total);
+    X.zflags_n = X.comb_flag_words(P, P.total);
     X.defer_double = true;   // itft + scale back to back
     X.fuse_row_last = true;  // last row level inside the pointwise (nested negacyclic sizes)
     ProfCall pc;
@@ -1703,7 +1733,7 @@ size_t mpfft_shard_combine_tmp_bytes(long n1, long n2, unsigned long depth, unsi
     Plan P;
     if (make_plan(&P, n1, n2, depth, w) || world < 1 || P.NC % world) return 0;
     const long sl = (long)((((u64)(P.NC / world) + 1) * P.bits1) / 64) + 2;
-    const long nb = P.Tr * Exec::comb_blocks(sl);
+    const long nb = P.Tr * Exec::comb_blocks(P, sl);
     return align_up((size_t)(nb + 1) * 4, 256) + align_up((size_t)nb * 4, 256);
 }
 
@@ -1729,14 +1759,14 @@ int mpfft_shard_combine(const mpfft_shard *sh, int phase, uint64_t *d_r, const u
     a.halo = d_halo;
     a.H = (int)H;
     a.SL = sl;
-    const long nb = nst * Exec::comb_blocks(sl);
+    const long nb = nst * Exec::comb_blocks(P, sl);
     u32 *st = (u32 *)d_tmp;
     u32 *allp = (u32 *)((unsigned char *)d_tmp + align_up((size_t)(nb + 1) * 4, 256));
     hipStream_t s = (hipStream_t)stream;
     if (phase == 0) {   // every stripe with carry-in 0, and its (generate, propagate) summary
         if ((rc = X.combine1(a, nst, sl, d_r, st, false, allp))) return rc;
         hipLaunchKernelGGL(k_comb_summary, dim3((unsigned)nst), dim3(256), 0, s, (const u32 *)st, (const u32 *)allp,
-                           Exec::comb_blocks(sl), d_sums);
+                           Exec::comb_blocks(P, sl), d_sums);
         HIPCHK(hipGetLastError());
         return MPFFT_OK;
     }

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 5, call O: k_combine1 consecutive form, the block's carry limb by the fixed-trip window;
+# 512-thread blocks (diag MPFFT_COMB_NT=512) and the per-limb form (MPFFT_COMB_CT=0) beside it.
+cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out && T=${1:-r5o} && \
+for r in 1 2; do
+  timeout -k 10 300 python3 -u bench.py --steps 40 --no-cpu-baseline --no-twin --e2e-reps 0 > gpurun_out/ab_${T}_c3_ct$r.log 2>&1 && \
+  MPFFT_LIB=diag MPFFT_COMB_NT=512 timeout -k 10 300 python3 -u bench.py --steps 40 --no-cpu-baseline --no-twin --e2e-reps 0 > gpurun_out/ab_${T}_c3_nt512_$r.log 2>&1 && \
+  MPFFT_LIB=diag MPFFT_COMB_CT=0 timeout -k 10 300 python3 -u bench.py --steps 40 --no-cpu-baseline --no-twin --e2e-reps 0 > gpurun_out/ab_${T}_c3_old$r.log 2>&1 && \
+  timeout -k 10 300 python3 -u bench.py --config C4 --steps 3 --warmup 1 --no-cpu-baseline --e2e-reps 0 --no-twin > gpurun_out/ab_${T}_c4_ct$r.log 2>&1 && \
+  MPFFT_LIB=diag MPFFT_COMB_NT=512 timeout -k 10 300 python3 -u bench.py --config C4 --steps 3 --warmup 1 --no-cpu-baseline --e2e-reps 0 --no-twin > gpurun_out/ab_${T}_c4_nt512_$r.log 2>&1 || exit 1
+done
+rc=$?; echo "rc=$rc"
+for f in gpurun_out/ab_${T}_*.log; do python3 -c "import json; d=json.loads([x for x in open('$f') if x.startswith('{')][-1]); s=d.get('stages_ms') or {}; print('$f', round(d['ms_per_step'],3), d.get('exact'), s.get('combine'), s.get('scale'))" 2>/dev/null; done
+exit $rc
