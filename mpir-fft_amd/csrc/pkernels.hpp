@@ -85,16 +85,16 @@ __host__ __device__ __forceinline__ int pw_norm(u64 (&L)[M], int T)
 {
     const int D = T + 1;
 #if defined(__HIP_DEVICE_COMPILE__)
-    // Fast path (the kernel is VALU-bound): a small D only moves the low word unless it
-    // under/overflows, which no lane of the wave does except with probability ~2^-30; then
-    // the top is -1 exactly.  Otherwise the full chain below.
+    // Device form (the kernel is VALU-bound): a small D only moves the low word unless it
+    // under/overflows (probability ~2^-32 per lane); such a lane keeps its top, which every
+    // reader handles (pw_combine's Tq != -1 branch) -- no full chain, whose rewrite of all M
+    // limbs under a branch made the compiler keep a second copy of L live across the levels'
+    // loop and spill it there (C4 pointwise 34.9 -> 34.1 ms, C3 3.47 -> 3.43 ms)
     {
         const u32 w0 = (u32)L[0], n0 = w0 - (u32)D;
         const bool spill = D > 0 ? w0 < (u32)D : (D < 0 ? n0 < (u32)(-D) : false);
-        if (!__any(spill)) {
-            L[0] = (L[0] & ~0xffffffffull) | n0;
-            return -1;
-        }
+        L[0] = (L[0] & ~0xffffffffull) | (spill ? w0 : n0);
+        return spill ? T : -1;
     }
 #endif
     const u32 dh = D < 0 ? ~0u : 0u;
@@ -393,6 +393,16 @@ __device__ __forceinline__ unsigned pw_mod(unsigned a, unsigned n)
 {
     a = a >= 2 * n ? a - 2 * n : a;
     return a >= n ? a - n : a;
+}
+
+// an opaque copy of the thread index: values derived from it are recomputed where used
+// instead of kept live across the transforms (cf. rp_launder)
+__device__ __forceinline__ int pw_launder(int t)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(t));
+#endif
+    return t;
 }
 
 // Exchange ordering inside one wave: a wave's LDS instructions execute in issue order, so a
@@ -732,9 +742,15 @@ __device__ __forceinline__ void pw_slot_product(u64 (&La)[M], int Ta, u64 (&Lb)[
     static_assert((N2 >> lk) << lk == N2, "omega must be a power of two");
     int Sa = 0, Sb = 0;                          // sign flags
     // negacyclic weight theta^t = 2^(t W2 / 2); a half-integer exponent (W2 and t odd) is
-    // 2^(floor(t W2 / 2) + N'/4) (2^(N'/2) - 1)  (sqrt 2 = 2^(N'/4) (2^(N'/2) - 1) in R')
+    // 2^(floor(t W2 / 2) + N'/4) (2^(N'/2) - 1)  (sqrt 2 = 2^(N'/4) (2^(N'/2) - 1) in R').
+    // Recomputed from an opaque copy of t where used again at l = 4096 (pw_launder): kept live
+    // from here to the un-weighting they took VGPRs that kernel spilled (144 -> 96 B per lane,
+    // C4 pointwise 35.8 -> 34.9 ms)
+    auto weight = [&](int tt) -> unsigned {
+        return (((unsigned)tt * W2) >> 1) + (((W2 & 1) && (tt & 1)) ? NP / 4 : 0);   // < N' + N'/4
+    };
     const bool half = (W2 & 1) && (t & 1);
-    unsigned Pa = (((unsigned)t * W2) >> 1) + (half ? NP / 4 : 0), Pb = Pa;   // < N' + N'/4
+    unsigned Pa = weight(t), Pb = late_b ? 0u : Pa;
     if (half) {
         pw_sqrt2<M>(La, Ta);
         if (!late_b) pw_sqrt2<M>(Lb, Tb);
@@ -744,7 +760,9 @@ __device__ __forceinline__ void pw_slot_product(u64 (&La)[M], int Ta, u64 (&Lb)[
     PW_STAMP(2);
     if constexpr (late_b) {
         loadB(Lb, Tb);
-        if (half) pw_sqrt2<M>(Lb, Tb);
+        const int tb = pw_launder(t);
+        Pb = weight(tb);
+        if ((W2 & 1) && (tb & 1)) pw_sqrt2<M>(Lb, Tb);
     }
     pw_transform<M, LK, 0>(Lb, Tb, Sb, Pb, Xw, TT, PP, W2, t);
     PW_STAMP(3);
@@ -774,9 +792,11 @@ __device__ __forceinline__ void pw_slot_product(u64 (&La)[M], int Ta, u64 (&Lb)[
     {
         // theta^-t 2^-lk: 2^-(t W2 / 2 + lk), for a half-integer t W2 / 2 (sqrt 2)^-1 = sqrt 2 / 2:
         // 2^(-floor(t W2 / 2) - 1 - lk + N'/4) (2^(N'/2) - 1)
-        const unsigned un = (((unsigned)t * W2) >> 1) + lk + (half ? 1 : 0);   // < N' + lk + 1
-        const unsigned F = pw_mod(Pz + N2 - un + (half ? NP / 4 : 0), N2);
-        if (half) pw_sqrt2<M>(Z, Tz);
+        const int tf = pw_tight(K) ? pw_launder(t) : t;   // (at l = 2048 the laundered form measured 1 % slower)
+        const bool halff = (W2 & 1) && (tf & 1);
+        const unsigned un = (((unsigned)tf * W2) >> 1) + lk + (halff ? 1 : 0);   // < N' + lk + 1
+        const unsigned F = pw_mod(Pz + N2 - un + (halff ? NP / 4 : 0), N2);
+        if (halff) pw_sqrt2<M>(Z, Tz);
         pw_publish<M, LK>(Z, Tz, Sz, Xw, pw_tight(K) ? nullptr : TT, t);
         pw_wave_sync();                                  // own column only
         pw_combine<M, LK, pw_pd<M, LK>()>(Z, Tz, Sz, 0, Xw, 2 * Tz + Sz, t, F);   // clears the sign flag
@@ -942,7 +962,11 @@ __global__ __launch_bounds__(1 << LK) __attribute__((amdgpu_waves_per_eu(pw_wpe<
         const int pos = (int)(slot & 3);
         pw_load_quad_bfly<M, CLP, K>(La, Ta, digA, cbA, topA, s0, pos, l, cbw, t);
         if (pw_late_b(K)) {
-            auto loadB = [&](u64 (&L)[M], int &T) { pw_load_quad_bfly<M, CLP, K>(L, T, digB, cbB, topB, s0, pos, l, cbw, t); };
+            // (an opaque copy of t: the piece offsets and mask bit positions of A's loader are not
+            // kept live across A's transform for reuse here)
+            auto loadB = [&](u64 (&L)[M], int &T) {
+                pw_load_quad_bfly<M, CLP, K>(L, T, digB, cbB, topB, s0, pos, l, cbw, pw_launder(t));
+            };
             pw_slot_product<M, LK>(La, Ta, Lb, Tb, X, Xw, TT, PP, t, stamp, loadB);
         } else {
             pw_load_quad_bfly<M, CLP, K>(Lb, Tb, digB, cbB, topB, s0, pos, l, cbw, t);
