@@ -507,7 +507,14 @@ __device__ __forceinline__ void pw_level(u64 (&L)[M], int &T, int &S, unsigned &
     if (cross) __syncthreads(); else pw_wave_sync();
 }
 
-template <int M, int LK, int DIR>
+// the highest compile-time-rotation level of operand B's transform in the late-B (l = 4096) form:
+// level 0 only -- while B transforms, A's transformed limbs are live, and the switch copies of
+// levels 1 and 2 pushed the kernel into spilling (96 -> 40 B per lane; C4 pointwise 34.0 -> 32.3 ms,
+// levels 0-1: 32.6; profiles/r05/pw_fixb_ab.txt).  A/B builds: -DPW_FIXB=1 / 2
+#ifndef PW_FIXB
+#define PW_FIXB 0
+#endif
+template <int M, int LK, int DIR, int FIXMAX = 2>
 __device__ __forceinline__ void pw_transform(u64 (&L)[M], int &T, int &S, unsigned &P, u32 *Xw, int *TT, unsigned *PP,
                                              unsigned W2, int t)
 {
@@ -526,9 +533,9 @@ __device__ __forceinline__ void pw_transform(u64 (&L)[M], int &T, int &S, unsign
         // inlined copy (peeled off the loop: one loop body with both forms spilled 3x more).
         static_assert(LK >= 7, "level 0's partner K/2 >= 64 lanes away");
         pw_level<M, LK, DIR, 0>(L, T, S, P, Xw, TT, PP, W2, t, 0);
-        if constexpr (LK >= 8) pw_level<M, LK, DIR, 1>(L, T, S, P, Xw, TT, PP, W2, t, 1);   // h = K/4 >= 64
-        if constexpr (LK >= 9) pw_level<M, LK, DIR, 2>(L, T, S, P, Xw, TT, PP, W2, t, 2);   // h = K/8 >= 64
-        jj = LK >= 9 ? 3 : LK >= 8 ? 2 : 1;
+        if constexpr (LK >= 8 && FIXMAX >= 1) pw_level<M, LK, DIR, 1>(L, T, S, P, Xw, TT, PP, W2, t, 1);   // h = K/4 >= 64
+        if constexpr (LK >= 9 && FIXMAX >= 2) pw_level<M, LK, DIR, 2>(L, T, S, P, Xw, TT, PP, W2, t, 2);   // h = K/8 >= 64
+        jj = LK >= 9 && FIXMAX >= 2 ? 3 : LK >= 8 && FIXMAX >= 1 ? 2 : 1;
     }
     for (; jj < LK; ++jj) pw_level<M, LK, DIR, -1>(L, T, S, P, Xw, TT, PP, W2, t, jj);
 }
@@ -764,7 +771,7 @@ __device__ __forceinline__ void pw_slot_product(u64 (&La)[M], int Ta, u64 (&Lb)[
         Pb = weight(tb);
         if ((W2 & 1) && (tb & 1)) pw_sqrt2<M>(Lb, Tb);
     }
-    pw_transform<M, LK, 0>(Lb, Tb, Sb, Pb, Xw, TT, PP, W2, t);
+    pw_transform<M, LK, 0, late_b ? PW_FIXB : 2>(Lb, Tb, Sb, Pb, Xw, TT, PP, W2, t);
     PW_STAMP(3);
 
     // ---- inner products: 2^Pa xa * 2^Pb xb = 2^(Pa + Pb) (xa xb) ---------------------

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5, call T: k_pwss register-pressure changes (laundered t for the weights and the late B loader, pw_norm without the full chain):
+# Round 5, call T: k_pwss register pressure (parity suite, C3 / C4 benches)
 # parity suite, C3 / C4 benches.
 cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out && T=${1:-r5t} && \
 timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_$T.log 2>&1 && \
