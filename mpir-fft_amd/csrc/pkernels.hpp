@@ -49,6 +49,12 @@ __host__ __device__ constexpr bool pw_tight(int K) { return PW_TIGHT9 && K == 51
 #define PW_LATE_B_ALL 0   // A/B builds: the late operand-B load at every size
 #endif
 __host__ __device__ constexpr bool pw_late_b(int K) { return pw_tight(K) || PW_LATE_B_ALL; }
+// inputs in flight in the late operand-B quad loader: one (A's transformed limbs are live; with two
+// the C4 kernel spilled 40 B per lane, with one it has no scratch at all, at equal speed:
+// C4 pointwise 32.41 vs 32.49 ms, profiles/r05/pw_late_infl_ab.txt).  A/B builds: -DPW_LATE_INFL=2
+#ifndef PW_LATE_INFL
+#define PW_LATE_INFL 1
+#endif
 #ifndef PW_QUAD4
 #define PW_QUAD4 0        // A/B builds: the quad loader's four inputs in flight at once
 #endif
@@ -675,7 +681,7 @@ __device__ __forceinline__ void pw_load_pair_bfly(u64 (&L)[M], int &T, const u64
 // Linear, so the pieces of z are signed sums of the inputs' pieces (|c_t| grows 4x: the inner
 // ring's headroom covers it, pdispatch.hpp).  Sums are kept in LP + 1 limbs two's complement,
 // one input piece formed at a time (registers), then sign-extended to M limbs.
-template <int M, int LP, int K>
+template <int M, int LP, int K, int INFL = 2>
 __device__ __forceinline__ void pw_load_quad_bfly(u64 (&L)[M], int &T, const u64 *dig, const u64 *cb, const int *top,
                                                   long s0, int pos, int l, int cbw, int t)
 {
@@ -713,6 +719,14 @@ __device__ __forceinline__ void pw_load_quad_bfly(u64 (&L)[M], int &T, const u64
         add(R2, 2, t);
         add(R1, 1, pr);
         add(R3, 3, pr);
+    } else if (INFL == 1) {   // one input's bytes at a time (x0, x2, x1, x3)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int q = u < 2 ? 2 * u : 2 * (u - 2) + 1, pt = (q & 1) && pos >= 2 ? tr : t;
+            PwRaw<LP> R;
+            pw_piece_fetch<LP>(R, dig + (size_t)(s0 + q) * l, cb + (size_t)(s0 + q) * cbw, top + s0 + q, l, pt);
+            add(R, q, pt);
+        }
     } else
     // two inputs' bytes in flight at a time (x0, x2 at piece t; then x1, x3)
 #pragma unroll
@@ -972,7 +986,7 @@ __global__ __launch_bounds__(1 << LK) __attribute__((amdgpu_waves_per_eu(pw_wpe<
             // (an opaque copy of t: the piece offsets and mask bit positions of A's loader are not
             // kept live across A's transform for reuse here)
             auto loadB = [&](u64 (&L)[M], int &T) {
-                pw_load_quad_bfly<M, CLP, K>(L, T, digB, cbB, topB, s0, pos, l, cbw, pw_launder(t));
+                pw_load_quad_bfly<M, CLP, K, PW_LATE_INFL>(L, T, digB, cbB, topB, s0, pos, l, cbw, pw_launder(t));
             };
             pw_slot_product<M, LK>(La, Ta, Lb, Tb, X, Xw, TT, PP, t, stamp, loadB);
         } else {
