@@ -520,6 +520,9 @@ __device__ __forceinline__ void pw_level(u64 (&L)[M], int &T, int &S, unsigned &
 #ifndef PW_FIXB
 #define PW_FIXB 0
 #endif
+#ifndef PW_FIXB_EARLY
+#define PW_FIXB_EARLY 2   // A/B builds: the same for operand B loaded with A (l <= 2048)
+#endif
 template <int M, int LK, int DIR, int FIXMAX = 2>
 __device__ __forceinline__ void pw_transform(u64 (&L)[M], int &T, int &S, unsigned &P, u32 *Xw, int *TT, unsigned *PP,
                                              unsigned W2, int t)
@@ -785,7 +788,7 @@ __device__ __forceinline__ void pw_slot_product(u64 (&La)[M], int Ta, u64 (&Lb)[
         Pb = weight(tb);
         if ((W2 & 1) && (tb & 1)) pw_sqrt2<M>(Lb, Tb);
     }
-    pw_transform<M, LK, 0, late_b ? PW_FIXB : 2>(Lb, Tb, Sb, Pb, Xw, TT, PP, W2, t);
+    pw_transform<M, LK, 0, late_b ? PW_FIXB : PW_FIXB_EARLY>(Lb, Tb, Sb, Pb, Xw, TT, PP, W2, t);
     PW_STAMP(3);
 
     // ---- inner products: 2^Pa xa * 2^Pb xb = 2^(Pa + Pb) (xa xb) ---------------------
