@@ -271,6 +271,27 @@ def multi_entry_line(mp, cfg, devices, steps, warmup, check=True, host_reps=1):
                                     "call (its own threaded packing, H2D, multiply, D2H of the stripes)")}
 
 
+def c_entry_child(cfg, G, share, steps, check, timeout=400):
+    """Rank 0's C-entry sub-record from a child process (`--mode multi`, no torch.distributed
+    environment): the cross-device peer path of mpfft_mul_multi has not run on separate GPUs
+    before a multi-GPU node takes it, so a fault or a hang there ends the child, not the rank
+    that prints the line."""
+    drop = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+            "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT")
+    env = {k: v for k, v in os.environ.items() if k not in drop and not k.startswith("TORCHELASTIC_")}
+    cmd = [sys.executable, os.path.abspath(__file__), "--mode", "multi", "--config", cfg, "--multi-ranks", str(G),
+           "--steps", str(steps), "--warmup", "1", "--e2e-reps", "1"]
+    cmd += (["--multi-share"] if share else []) + ([] if check else ["--no-check"])
+    try:
+        p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+    except subprocess.TimeoutExpired:
+        return {"error": f"the C entry did not finish within {timeout} s (child killed)"}
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"error": f"child exit status {p.returncode}", "stderr_tail": p.stderr[-800:]}
+    return json.loads(lines[-1])
+
+
 def golden_digest(cfg):
     p = os.path.join(ROOT, "tests", "golden", "products.json")
     try:
@@ -388,12 +409,8 @@ def main():
                 # the same product through the one-process C entry over devices 0 .. N-1 (the
                 # other ranks wait at the barrier below): a transport failure in one driver still
                 # leaves a curve from the other
-                try:
-                    devs = [0] * world if share else list(range(world))
-                    res["c_entry"] = multi_entry_line(mp, cfg, devs, max(1, min(args.steps, 3)), 1,
-                                                      check=not args.no_check)
-                except Exception as e:   # reported, never fatal to the rank-level line
-                    res["c_entry"] = {"error": repr(e)}
+                torch.cuda.empty_cache()
+                res["c_entry"] = c_entry_child(cfg, world, share, max(1, min(args.steps, 3)), not args.no_check)
             print(json.dumps(res))
         if world > 1:
             dist.barrier(group=host_pg)
