@@ -292,6 +292,21 @@ def c_entry_child(cfg, G, share, steps, check, timeout=400):
     return json.loads(lines[-1])
 
 
+def c_entry_fallback_line(args, cfg, world, c_entry, err):
+    """The N > 1 line when sharded.py raised on rank 0: the same C4 product over the same N
+    devices through the one-process C entry (mpfft_mul_multi_device), with the failure named."""
+    depth, w, nl = CONFIGS[cfg]
+    ok = isinstance(c_entry, dict) and "value" in c_entry
+    return {"metric": METRIC, "value": c_entry["value"] if ok else None, "unit": "limbs/s", "n_gpus": world,
+            "steps": c_entry.get("steps") if ok else 0, "warmup": 1,
+            "ms_per_step": c_entry["ms_per_step"] if ok else None, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic (xoshiro256** limbs, seeds 0x1001/0x2002)",
+            "config": {"workload": f"{cfg}: new_mpn_mul depth={depth} w={w} n1=n2={nl} limbs over {world} devices",
+                       "parallelism": f"MFA columns x{world} through the one-process C entry (torch.distributed run failed)"},
+            "exact": c_entry.get("exact") if ok else None, "sharded_error": err, "c_entry": c_entry}
+
+
 def golden_digest(cfg):
     p = os.path.join(ROOT, "tests", "golden", "products.json")
     try:
@@ -397,20 +412,30 @@ def main():
             twin = single_gpu_line(mp, dev, cfg, 3, 1, check=not args.no_check)
         if world > 1:
             dist.barrier()
-        res = sh.bench(args, cfg, CONFIGS[cfg], rank, world, dev)
+        try:
+            if os.environ.get("MPFFT_BENCH_FAIL_SHARDED") == "1":   # rehearsal of the fallback below
+                raise RuntimeError("MPFFT_BENCH_FAIL_SHARDED=1")
+            res, sharded_err = sh.bench(args, cfg, CONFIGS[cfg], rank, world, dev), None
+        except Exception as e:   # reported on the line; rank 0 then falls back to the C entry's curve
+            res, sharded_err = None, repr(e)
         # the other ranks wait on a host-side (gloo) barrier while rank 0 times the C entry on
         # their devices: an RCCL barrier would leave a kernel spinning on each of those GPUs
         host_pg = dist.new_group(backend="gloo") if world > 1 else None
         if world > 1:
             dist.barrier(group=host_pg)
         if rank == 0:
-            res["n1_twin"] = twin
-            if not args.no_c_entry:
+            c_entry = None
+            if not args.no_c_entry or res is None:
                 # the same product through the one-process C entry over devices 0 .. N-1 (the
                 # other ranks wait at the barrier below): a transport failure in one driver still
                 # leaves a curve from the other
                 torch.cuda.empty_cache()
-                res["c_entry"] = c_entry_child(cfg, world, share, max(1, min(args.steps, 3)), not args.no_check)
+                c_entry = c_entry_child(cfg, world, share, max(1, min(args.steps, 3)), not args.no_check)
+            if res is None:   # the torch.distributed run failed on this rank: the C entry's line
+                res = c_entry_fallback_line(args, cfg, world, c_entry, sharded_err)
+            else:
+                res["c_entry"] = c_entry
+            res["n1_twin"] = twin
             print(json.dumps(res))
         if world > 1:
             dist.barrier(group=host_pg)
