@@ -77,7 +77,10 @@ __host__ __device__ constexpr int pw_wpe()
 #define PW_PD_TIGHT 16
 #endif
 template <int M, int LK>
-__host__ __device__ constexpr int pw_pd() { return pw_wpe<M, LK>() == 4 ? (pw_tight(1 << LK) ? PW_PD_TIGHT : 16) : 2 * M; }
+#ifndef PW_PD_WIDE
+#define PW_PD_WIDE 16     // A/B builds: the same for the K = 256 kernels
+#endif
+__host__ __device__ constexpr int pw_pd() { return pw_wpe<M, LK>() == 4 ? (pw_tight(1 << LK) ? PW_PD_TIGHT : PW_PD_WIDE) : 2 * M; }
 
 // Exchange format: thread t publishes its value as 2M 32-bit words, word k at
 // Xw[k K + t] (conflict-free for any rotation), top in TT[t].  Before publishing,
