@@ -872,26 +872,34 @@ __device__ __forceinline__ void pw_slot_output(const u64 *X, const int *TT, int 
         if (r >= RPT) continue;
         const int m = t + NTH * r;
         i128 S = 0;
-        // pieces whose limbs [t'LP, t'LP + M] cover m, directly and through the wrap (m + l)
-#pragma unroll
-        for (int wrap = 0; wrap < 2; ++wrap) {
-            const int mm = m + wrap * l;
-            int lo = (mm - M + LP - 1) / LP;       // ceil((mm - M) / LP) for mm >= M
-            if (mm < M) lo = 0;
-            int hi = mm / LP;
-            if (hi > K - 1) hi = K - 1;
-            for (int tp = lo; tp <= hi; ++tp) {
-                const int d = mm - tp * LP;        // limb of c_tp, 0 .. M
-                i128 v;
-                if (pw_tight(K)) {                 // two's complement: limb M is the sign extension
-                    v = d < M ? (i128)X[(size_t)d * K + tp] : -(i128)(X[(size_t)(M - 1) * K + tp] >> 63);
-                } else {
-                    const int tt = TT[tp];
-                    v = d < M ? (i128)X[(size_t)d * K + tp] : (i128)(tt >> 1);
-                    if ((tt & 1) && (d == 0 || d == M)) v -= 1;
-                }
-                S += wrap ? -v : v;
+        // limb d of c_tp (0 .. M): two's complement in the tight form (limb M the sign extension)
+        auto limb_of = [&](int d, int tp) -> i128 {
+            i128 v;
+            if (pw_tight(K)) {
+                v = d < M ? (i128)X[(size_t)d * K + tp] : -(i128)(X[(size_t)(M - 1) * K + tp] >> 63);
+            } else {
+                const int tt = TT[tp];
+                v = d < M ? (i128)X[(size_t)d * K + tp] : (i128)(tt >> 1);
+                if ((tt & 1) && (d == 0 || d == M)) v -= 1;
             }
+            return v;
+        };
+        // pieces whose limbs [t'LP, t'LP + M] cover m: t' = m / LP - j, j < M / LP + 1 -- a
+        // fixed-trip loop of guarded reads (a runtime-bounded one serialised its LDS round trips)
+        {
+            constexpr int LPc = pw_piece_limbs<M, LK>(), KP = M / LPc + 1;
+            const int hi = m / LPc;
+#pragma unroll
+            for (int j = 0; j < KP; ++j) {
+                const int tp = hi - j, d = m - tp * LPc;
+                if (tp >= 0 && d <= M) S += limb_of(d, tp);
+            }
+        }
+        // ... and through the wrap (limb m + l, negated): only m < M
+        if (m < M) {
+            const int mm = m + l;
+            int lo = (mm - M + LP - 1) / LP;
+            for (int tp = lo; tp <= K - 1; ++tp) S -= limb_of(mm - tp * LP, tp);
         }
         fo[r] = (u64)S;
         ho[r] = (int)(i64)(S >> 64);
