@@ -55,6 +55,9 @@ __host__ __device__ constexpr bool pw_late_b(int K) { return pw_tight(K) || PW_L
 #ifndef PW_LATE_INFL
 #define PW_LATE_INFL 1
 #endif
+#ifndef PW_A_INFL
+#define PW_A_INFL 2       // A/B builds: inputs in flight in operand A's quad loader (1, 2 or 4)
+#endif
 #ifndef PW_QUAD4
 #define PW_QUAD4 0        // A/B builds: the quad loader's four inputs in flight at once
 #endif
@@ -714,7 +717,7 @@ __device__ __forceinline__ void pw_load_quad_bfly(u64 (&L)[M], int &T, const u64
             acc[j] = ((u64)hi << 32) | lo;
         }
     };
-    if (PW_QUAD4) {   // all four inputs' bytes in flight at once
+    if (PW_QUAD4 || INFL == 4) {   // all four inputs' bytes in flight at once
         const int pr = pos >= 2 ? tr : t;
         PwRaw<LP> R0, R1, R2, R3;
         pw_piece_fetch<LP>(R0, dig + (size_t)s0 * l, cb + (size_t)s0 * cbw, top + s0, l, t);
@@ -995,7 +998,7 @@ __global__ __launch_bounds__(1 << LK) __attribute__((amdgpu_waves_per_eu(pw_wpe<
         }
         const long s0 = slot & ~3L;
         const int pos = (int)(slot & 3);
-        pw_load_quad_bfly<M, CLP, K>(La, Ta, digA, cbA, topA, s0, pos, l, cbw, t);
+        pw_load_quad_bfly<M, CLP, K, PW_A_INFL>(La, Ta, digA, cbA, topA, s0, pos, l, cbw, t);
         if (pw_late_b(K)) {
             // (an opaque copy of t: the piece offsets and mask bit positions of A's loader are not
             // kept live across A's transform for reuse here)
