@@ -109,6 +109,11 @@ int mpfft_workspace_layout(long n1, long n2, unsigned long depth, unsigned long 
 #define MPFFT_STAGE_SCALE 5         /* divide by 2^(depth+1), normalise               (mul_fft.c:3256-3260) */
 #define MPFFT_STAGE_COMBINE 6       /* FFT_combine_bits                               (mul_fft.c:3261-3262) */
 #define MPFFT_NSTAGES 7
+/* (tests) the folded path's combine: the workspace's coefficients as the inverse
+ * columns leave them -- reduced form, 2^-(depth+1) already applied, the rows the truncated
+ * inverse doubles not yet doubled -- into the product; MPFFT_EUNSUPPORTED on plans that do not
+ * fold (mpfft_stage_kernels names k_combine_red for them) */
+#define MPFFT_STAGE_FOLD_COMBINE 7
 int mpfft_stage(int stage, const uint64_t *d_i1, const uint64_t *d_i2, uint64_t *d_r, long n1, long n2,
                 unsigned long depth, unsigned long w, void *d_ws, size_t ws_bytes, void *stream);
 
@@ -247,6 +252,13 @@ int mpfft_mul_multi_device(long n1, long n2, unsigned long depth, unsigned long 
                            const uint64_t *const *d_src1, const uint64_t *const *d_src2, uint64_t *const *d_r,
                            void *const *streams);
 int mpfft_multi_release(void);
+/* The event graph of `calls` back-to-back mpfft_mul_multi_device calls over `world` ranks, as
+ * text (no GPU touched, nothing allocated): one line per cross-stream ordering and per queued
+ * piece of work -- "R d S ev" record, "W d S e ev" wait, "K d S what" rank-local work,
+ * "C d S what e" a copy from rank e, "N" next call (multi.hip, the event graph).  Returns the
+ * bytes needed including the terminating 0 (buf may be null), or a negative MPFFT_E* code. */
+long mpfft_multi_schedule(long n1, long n2, unsigned long depth, unsigned long w, int world, int calls, char *buf,
+                          size_t len);
 
 /* new_mpn_mul / mpfft_mul_ex policy: with ngpus > 1 devices set, products whose coefficients
  * have >= min_l limbs (0: 1024) and whose NC the device count divides run through

@@ -26,7 +26,7 @@ LIB_PATH = os.path.join(_HERE, "libmpfft_diag.so" if _LIBSEL == "diag" else
 _lib = None
 
 STAGE_FWD_COLUMNS, STAGE_FWD_ROWS, STAGE_POINTWISE, STAGE_INV_ROWS, STAGE_INV_COLUMNS, \
-    STAGE_SCALE, STAGE_COMBINE = range(7)
+    STAGE_SCALE, STAGE_COMBINE, STAGE_FOLD_COMBINE = range(8)
 
 _u64p = ctypes.POINTER(ctypes.c_uint64)
 _vp = ctypes.c_void_p
@@ -142,6 +142,10 @@ def lib():
         h.mpfft_mul_multi.restype = ctypes.c_int
         h.mpfft_multi_release.argtypes = []
         h.mpfft_multi_release.restype = ctypes.c_int
+        if hasattr(h, "mpfft_multi_schedule"):   # (older libraries in A/B runs lack it)
+            h.mpfft_multi_schedule.argtypes = [_L, _L, _UL, _UL, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                                               ctypes.c_size_t]
+            h.mpfft_multi_schedule.restype = ctypes.c_long
         h.mpfft_set_devices.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), _L]
         h.mpfft_set_devices.restype = ctypes.c_int
         h.mpfft_last_ngpus.argtypes = []
@@ -543,3 +547,18 @@ def set_devices(devices, min_l=0):
 
 def multi_release():
     return lib().mpfft_multi_release()
+
+
+def multi_schedule(n1, n2, depth, w, world, calls=1):
+    """The event graph of `calls` back-to-back device-resident multi-rank multiplies
+    (mpfft_multi_schedule: a dry run, no GPU): list of (kind, rank, stream, *rest) tuples."""
+    n = lib().mpfft_multi_schedule(n1, n2, depth, w, world, calls, None, 0)
+    if n < 0:
+        raise MpfftError(-n, "multi_schedule")
+    buf = ctypes.create_string_buffer(n)
+    lib().mpfft_multi_schedule(n1, n2, depth, w, world, calls, buf, n)
+    out = []
+    for line in buf.value.decode().splitlines():
+        f = line.split()
+        out.append(tuple([f[0]] + [int(x) if x.lstrip("-").isdigit() else x for x in f[1:]]))
+    return out

@@ -590,19 +590,6 @@ __device__ __forceinline__ u64 src_limb(const u64 *src, long nsrc, const SrcSlic
     return r < v.chunk ? src[p * v.chunk + r] : 0;
 }
 
-// src_limb without guarded loads: the limb is read from a clamped, always valid address (limb 0
-// of a non-empty operand) and zeroed after, so a kernel can put many of these loads in flight
-// at once (a guarded load is a branch, and the compiler waits for its loads at the join)
-__device__ __forceinline__ u64 src_limb_nb(const u64 *src, long nsrc, const SrcSlice &v, long j, u64 bits1, long q)
-{
-    const long p = j >> __builtin_ctzl((unsigned long)v.NC);
-    const long r = q - (long)(((u64)(p * v.NC + v.c0) * bits1) >> 6);
-    const bool ok = q < nsrc && (!v.chunk || r < v.chunk);
-    const long idx = v.chunk ? p * v.chunk + r : q;
-    const u64 w = src[ok ? idx : 0];
-    return ok ? w : 0;
-}
-
 // Fused split (FFT_split_bits, mul_fft.c:115-170): coefficient j is the bits1-bit
 // chunk at bit offset j*bits1 of the operand (bits past its end read as 0).
 template <int U>

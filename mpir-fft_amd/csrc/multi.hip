@@ -35,8 +35,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <stdarg.h>
+
 #include <algorithm>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -254,6 +257,9 @@ struct Rank {
     hipStream_t xs = nullptr;    // exchange #1's copies (overlapping operand 2's column passes)
     hipEvent_t eva = nullptr;    // operand 1's column passes done
     hipEvent_t evx = nullptr;    // exchange #1 done
+    hipEvent_t evs = nullptr;    // combine phase 0 done: this rank's stripe summaries are ready
+    hipEvent_t evd = nullptr;    // this rank's whole call done (every pull it made is complete)
+    bool done_rec = false;       // evd recorded by an earlier call
     unsigned char *mem = nullptr;
     size_t mem_bytes = 0;
     u64 *host = nullptr;      // pinned staging of the operand slices
@@ -288,6 +294,63 @@ Ctx g_ctx;
 
 #define MCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { mpfft_note_hip_error(e_); return MPFFT_EHIP; } } while (0)
 
+// ---- the event graph ------------------------------------------------------------------------
+// Every cross-stream ordering in run_ranks goes through rec() / wait() and every queued piece of
+// work through work() / copy_from(): with a schedule trace active they also append one line to
+// it, and in a dry run (mpfft_multi_schedule) they do only that -- no HIP call, no memory -- so
+// the CPU tests check the event graph itself (tests/test_multi_schedule.py):
+//   R d S E       record rank d's event E on its stream S (s: compute, x: exchange #1)
+//   W d S e E     rank d's stream S waits for rank e's event E (its most recent record)
+//   K d S what    work on rank d's stream S that touches rank d's buffers only
+//   C d S what e  a copy on rank d's stream S reading rank e's buffers into rank d's
+//   N             the next call
+enum { EV_MAIN, EV_A, EV_X, EV_SUM, EV_DONE };
+const char *const ev_names[] = {"ev", "eva", "evx", "evs", "evd"};
+struct Sched {
+    std::string log;
+    bool dry = false;
+};
+thread_local Sched *g_sched = nullptr;
+bool dry() { return g_sched && g_sched->dry; }
+void sched_line(const char *fmt, ...)
+{
+    if (!g_sched) return;
+    char b[160];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(b, sizeof(b), fmt, ap);
+    va_end(ap);
+    g_sched->log += b;
+    g_sched->log += '\n';
+}
+hipEvent_t ev_of(const Rank &R, int e)
+{
+    return e == EV_MAIN ? R.ev : e == EV_A ? R.eva : e == EV_X ? R.evx : e == EV_SUM ? R.evs : R.evd;
+}
+#define SETDEV(R) do { if (!dry()) MCHK(hipSetDevice((R).dev)); } while (0)
+int rec(std::vector<Rank> &rk, int d, int e, bool xs = false)
+{
+    sched_line("R %d %c %s", d, xs ? 'x' : 's', ev_names[e]);
+    if (!dry()) MCHK(hipEventRecord(ev_of(rk[d], e), xs ? rk[d].xs : rk[d].s));
+    return MPFFT_OK;
+}
+int wait(std::vector<Rank> &rk, int d, bool xs, int e, int ev)
+{
+    sched_line("W %d %c %d %s", d, xs ? 'x' : 's', e, ev_names[ev]);
+    if (!dry()) MCHK(hipStreamWaitEvent(xs ? rk[d].xs : rk[d].s, ev_of(rk[e], ev), 0));
+    return MPFFT_OK;
+}
+bool work(int d, bool xs, const char *what)   // false: a dry run (skip the HIP call)
+{
+    sched_line("K %d %c %s", d, xs ? 'x' : 's', what);
+    return !dry();
+}
+bool copy_from(int d, bool xs, const char *what, int src)
+{
+    sched_line("C %d %c %s %d", d, xs ? 'x' : 's', what, src);
+    return !dry();
+}
+
 size_t al(size_t x) { return (x + 255) / 256 * 256; }
 
 // wait for every stream of every rank: no copy engine may still read or write a buffer
@@ -311,21 +374,16 @@ void free_rank(Rank &R)
     if (R.ev) (void)hipEventDestroy(R.ev);
     if (R.eva) (void)hipEventDestroy(R.eva);
     if (R.evx) (void)hipEventDestroy(R.evx);
+    if (R.evs) (void)hipEventDestroy(R.evs);
+    if (R.evd) (void)hipEventDestroy(R.evd);
     if (R.s) (void)hipStreamDestroy(R.s);
     if (R.xs) (void)hipStreamDestroy(R.xs);
     R = Rank();
 }
 
-// carve rank d's arrays out of one grow-only allocation (host: also the operand slices, their
-// pinned staging and the product stripes)
-int setup_rank(const Part &p, int d, Rank &R, bool host, const HaloRank &HR)
+// rank d's device bytes (one grow-only allocation) and pinned host bytes for partition p
+size_t rank_need(const Part &p, int d, bool host, const HaloRank &HR, size_t *host_bytes)
 {
-    MCHK(hipSetDevice(R.dev));
-    if (!R.s) MCHK(hipStreamCreateWithFlags(&R.s, hipStreamNonBlocking));
-    if (!R.ev) MCHK(hipEventCreateWithFlags(&R.ev, hipEventDisableTiming));
-    if (!R.xs) MCHK(hipStreamCreateWithFlags(&R.xs, hipStreamNonBlocking));
-    if (!R.eva) MCHK(hipEventCreateWithFlags(&R.eva, hipEventDisableTiming));
-    if (!R.evx) MCHK(hipEventCreateWithFlags(&R.evx, hipEventDisableTiming));
     const long cs = p.NR * p.C, rs = p.rcount(d) * p.NC;
     const bool w1 = p.world == 1;
     const int ncol = (w1 && p.fused) ? 3 : 2;          // world 1: the fused product's column array
@@ -335,10 +393,33 @@ int setup_rank(const Part &p, int d, Rank &R, bool host, const HaloRank &HR)
     // the host entry's device copies of its operands: the rank's slices, or the whole operands
     // when every rank computes every column block (no packing: straight H2D)
     const long s1 = p.rep ? p.n1 : p.src_limbs(), s2 = p.rep ? p.n2 : p.src_limbs();
-    const size_t need = ncol * arr_bytes(cs) + nrow * arr_bytes(rs) + (host ? al(s1 * 8) + al(s2 * 8) + al(p.Tr * p.SL * 8) : 0) +
-                        al(p.Tr * p.H * p.l * 8) + al(p.Tr * 2 * 4) + al(p.world * p.Tr * 2 * 4) + al(ctb) +
-                        al(HR.send_n * 8) + al(HR.stage_n * 8) + al(HR.pack.size() * sizeof(Run)) +
-                        al(HR.scatter.size() * sizeof(Run)) + 256;
+    *host_bytes = host ? (size_t)std::max<long>(p.rep ? 0 : 2 * p.src_limbs(), p.Tr * p.SL) * 8 : 0;
+    return ncol * arr_bytes(cs) + nrow * arr_bytes(rs) + (host ? al(s1 * 8) + al(s2 * 8) + al(p.Tr * p.SL * 8) : 0) +
+           al(p.Tr * p.H * p.l * 8) + al(p.Tr * 2 * 4) + al(p.world * p.Tr * 2 * 4) + al(ctb) +
+           al(HR.send_n * 8) + al(HR.stage_n * 8) + al(HR.pack.size() * sizeof(Run)) +
+           al(HR.scatter.size() * sizeof(Run)) + 256;
+}
+
+// carve rank d's arrays out of one grow-only allocation (host: also the operand slices, their
+// pinned staging and the product stripes).  A reallocation frees memory other ranks' streams
+// may still pull from: prepare() drains every rank first when any of them grows.
+int setup_rank(const Part &p, int d, Rank &R, bool host, const HaloRank &HR)
+{
+    MCHK(hipSetDevice(R.dev));
+    if (!R.s) MCHK(hipStreamCreateWithFlags(&R.s, hipStreamNonBlocking));
+    if (!R.ev) MCHK(hipEventCreateWithFlags(&R.ev, hipEventDisableTiming));
+    if (!R.xs) MCHK(hipStreamCreateWithFlags(&R.xs, hipStreamNonBlocking));
+    if (!R.eva) MCHK(hipEventCreateWithFlags(&R.eva, hipEventDisableTiming));
+    if (!R.evx) MCHK(hipEventCreateWithFlags(&R.evx, hipEventDisableTiming));
+    if (!R.evs) MCHK(hipEventCreateWithFlags(&R.evs, hipEventDisableTiming));
+    if (!R.evd) MCHK(hipEventCreateWithFlags(&R.evd, hipEventDisableTiming));
+    const long cs = p.NR * p.C, rs = p.rcount(d) * p.NC;
+    const bool w1 = p.world == 1;
+    const int ncol = (w1 && p.fused) ? 3 : 2;
+    const long s1 = p.rep ? p.n1 : p.src_limbs(), s2 = p.rep ? p.n2 : p.src_limbs();
+    size_t hb = 0;
+    const size_t need = rank_need(p, d, host, HR, &hb);
+    const size_t ctb = mpfft_shard_combine_tmp_bytes(p.n1, p.n2, p.depth, p.w, p.world);
     if (R.mem_bytes < need) {
         if (R.mem) {
             (void)hipStreamSynchronize(R.s);
@@ -397,8 +478,7 @@ int setup_rank(const Part &p, int d, Rank &R, bool host, const HaloRank &HR)
         R.src[0] = (u64 *)q; q += al(s1 * 8);
         R.src[1] = (u64 *)q; q += al(s2 * 8);
         R.r = (u64 *)q; q += al(p.Tr * p.SL * 8);
-        // pinned staging: the packed slices on the way in, the stripes on the way out
-        const size_t hb = (size_t)std::max<long>(p.rep ? 0 : 2 * p.src_limbs(), p.Tr * p.SL) * 8;
+        // pinned staging: the packed slices on the way in, the stripes on the way out (hb)
         if (R.host_bytes < hb) {
             if (R.host) MCHK(hipHostFree(R.host));
             R.host = nullptr;
@@ -479,17 +559,34 @@ void *loc(const Rank &R, int layout, int op, int field, long off)
     return field_ptr(layout ? R.row[op] : R.col[op], field, off);
 }
 
-// queue one copy of an exchange or halo plan on stream `st` of its receiving rank
-int queue_copy(const std::vector<Rank> &rk, const mpfft_copy &c, hipStream_t st)
+// queue one copy of an exchange or halo plan on its receiving rank's stream (xs: the exchange
+// stream)
+int queue_copy(std::vector<Rank> &rk, const mpfft_copy &c, bool xs, const char *what)
 {
     const Rank &S = rk[c.src], &D = rk[c.dst];
     const size_t es = c.field == 2 ? 4 : 8;
     void *dp = loc(D, c.dst_layout, c.op, c.field, c.dst_off);
     const void *sp = loc(S, c.src_layout, c.op, c.field, c.src_off);
-    if (dp == sp) return MPFFT_OK;   // world 1: the row layout is a view of the column layout
+    if (!dry() && dp == sp) return MPFFT_OK;   // world 1: the row layout is a view of the column layout
+    if (!copy_from(c.dst, xs, what, c.src)) return MPFFT_OK;
+    const hipStream_t st = xs ? D.xs : D.s;
     if (S.dev == D.dev) MCHK(hipMemcpyAsync(dp, sp, c.count * es, hipMemcpyDeviceToDevice, st));
     else MCHK(hipMemcpyPeerAsync(dp, D.dev, sp, S.dev, c.count * es, st));
     return MPFFT_OK;
+}
+
+const char *shard_stage_name(int stage)
+{
+    switch (stage) {
+    case MPFFT_SHARD_FWD_COLUMNS_A: return "fwd_columns_a";
+    case MPFFT_SHARD_FWD_COLUMNS_B: return "fwd_columns_b";
+    case MPFFT_SHARD_FWD_COLUMNS_OWN: return "fwd_columns_own";
+    case MPFFT_SHARD_FWD_ROWS: return "fwd_rows";
+    case MPFFT_SHARD_POINTWISE: return "pointwise";
+    case MPFFT_SHARD_INV_ROWS: return "inv_rows";
+    case MPFFT_SHARD_INV_COLUMNS: return "inv_columns";
+    }
+    return "stage";
 }
 
 // replicated forward columns (world 2): rank d runs every column block e's split + column
@@ -504,21 +601,23 @@ int fwd_replicated(const Part &p, std::vector<Rank> &rk, unsigned long depth, un
     const long sl = p.Tr * p.chunk;
     for (int d = 0; d < p.world; ++d) {
         Rank &R = rk[d];
-        MCHK(hipSetDevice(R.dev));
+        SETDEV(R);
         for (int e = 0; e < p.world; ++e) {
             mpfft_shard sh = desc(p, d, R, depth, w);
             sh.c0 = (int)(e * p.C);
             const long o = R.whole ? 0 : e * sl;   // block e's slices, or the whole operands
-            int rc = mpfft_shard_stage(MPFFT_SHARD_FWD_COLUMNS_OWN, &sh, R.in[0] + o, R.in[1] + o, R.s);
-            if (rc) return rc;
+            int rc;
+            if (work(d, false, shard_stage_name(MPFFT_SHARD_FWD_COLUMNS_OWN)) &&
+                (rc = mpfft_shard_stage(MPFFT_SHARD_FWD_COLUMNS_OWN, &sh, R.in[0] + o, R.in[1] + o, R.s)))
+                return rc;
             for (const mpfft_copy &c : plan)
                 if (c.dst == d && c.src == e) {
                     mpfft_copy m = c;
                     m.src = d;          // block e's column layout is rank d's own column arrays now
-                    if ((rc = queue_copy(rk, m, R.s))) return rc;
+                    if ((rc = queue_copy(rk, m, false, "xchg1_local"))) return rc;
                 }
         }
-        MCHK(hipEventRecord(R.ev, R.s));
+        if (int rc = rec(rk, d, EV_MAIN)) return rc;
     }
     return MPFFT_OK;
 }
@@ -531,44 +630,41 @@ int run_exchange_fwd(const Part &p, std::vector<Rank> &rk)
 {
     std::vector<mpfft_copy> plan;
     exchange_plan(p, MPFFT_XCHG_COL_TO_ROW, plan);
+    int rc;
     for (int d = 0; d < p.world; ++d) {
-        Rank &D = rk[d];
-        MCHK(hipSetDevice(D.dev));
+        SETDEV(rk[d]);
         for (int op = 0; op < 2; ++op) {
-            for (int s = 0; s < p.world; ++s) MCHK(hipStreamWaitEvent(D.xs, op ? rk[s].ev : rk[s].eva, 0));
+            for (int s = 0; s < p.world; ++s)
+                if ((rc = wait(rk, d, true, s, op ? EV_MAIN : EV_A))) return rc;
             for (const mpfft_copy &c : plan)
-                if (c.dst == d && c.op == op) {
-                    int rc = queue_copy(rk, c, D.xs);
-                    if (rc) return rc;
-                }
+                if (c.dst == d && c.op == op && (rc = queue_copy(rk, c, true, "xchg1"))) return rc;
         }
-        MCHK(hipEventRecord(D.evx, D.xs));
+        if ((rc = rec(rk, d, EV_X, true))) return rc;
     }
     for (int d = 0; d < p.world; ++d) {   // senders' compute streams must not run ahead of the pulls
-        MCHK(hipSetDevice(rk[d].dev));
-        for (int s = 0; s < p.world; ++s) MCHK(hipStreamWaitEvent(rk[d].s, rk[s].evx, 0));
-        MCHK(hipEventRecord(rk[d].ev, rk[d].s));
+        SETDEV(rk[d]);
+        for (int s = 0; s < p.world; ++s)
+            if ((rc = wait(rk, d, false, s, EV_X))) return rc;
+        if ((rc = rec(rk, d, EV_MAIN))) return rc;
     }
     return MPFFT_OK;
 }
 
 // queue a set of copies (an exchange or the halo): each receiver waits for every sender's last
-// event, then pulls
-int run_copies(const Part &p, std::vector<Rank> &rk, const std::vector<mpfft_copy> &plan)
+// event, then pulls; the events are re-recorded only after every receiver queued its waits
+int run_copies(const Part &p, std::vector<Rank> &rk, const std::vector<mpfft_copy> &plan, const char *what)
 {
+    int rc;
     for (int d = 0; d < p.world; ++d) {
-        MCHK(hipSetDevice(rk[d].dev));
+        SETDEV(rk[d]);
         for (int s = 0; s < p.world; ++s)
-            if (s != d) MCHK(hipStreamWaitEvent(rk[d].s, rk[s].ev, 0));
-        for (const mpfft_copy &c : plan) {
-            if (c.dst != d) continue;
-            int rc = queue_copy(rk, c, rk[d].s);
-            if (rc) return rc;
-        }
+            if (s != d && (rc = wait(rk, d, false, s, EV_MAIN))) return rc;
+        for (const mpfft_copy &c : plan)
+            if (c.dst == d && (rc = queue_copy(rk, c, false, what))) return rc;
     }
     for (int d = 0; d < p.world; ++d) {
-        MCHK(hipSetDevice(rk[d].dev));
-        MCHK(hipEventRecord(rk[d].ev, rk[d].s));
+        SETDEV(rk[d]);
+        if ((rc = rec(rk, d, EV_MAIN))) return rc;
     }
     return MPFFT_OK;
 }
@@ -578,15 +674,16 @@ int stage_all(const Part &p, std::vector<Rank> &rk, int stage, unsigned long dep
 {
     for (int d = 0; d < p.world; ++d) {
         Rank &R = rk[d];
-        MCHK(hipSetDevice(R.dev));
+        SETDEV(R);
         const mpfft_shard sh = desc(p, d, R, depth, w);
-        int rc = mpfft_shard_stage(stage, &sh, R.in[0], R.in[1], R.s);
-        if (rc) return rc;
+        int rc;
+        if (work(d, false, shard_stage_name(stage)) && (rc = mpfft_shard_stage(stage, &sh, R.in[0], R.in[1], R.s)))
+            return rc;
         if (stage == MPFFT_SHARD_POINTWISE && p.fused) {   // the product is in rowc: operand 0 from here on
             std::swap(R.row[0], R.rowc);
             if (p.world == 1) std::swap(R.col[0], R.colc);
         }
-        MCHK(hipEventRecord(ev_a ? R.eva : R.ev, R.s));
+        if ((rc = rec(rk, d, ev_a ? EV_A : EV_MAIN))) return rc;
     }
     return MPFFT_OK;
 }
@@ -595,48 +692,65 @@ int stage_all(const Part &p, std::vector<Rank> &rk, int stage, unsigned long dep
 // per sender after that sender's pack, and scatters the blocks that are not contiguous in its halo
 int run_halo(const Part &p, std::vector<Rank> &rk, const std::vector<HaloRank> &hr)
 {
+    int rc;
     for (int s = 0; s < p.world; ++s) {
         Rank &S = rk[s];
-        MCHK(hipSetDevice(S.dev));
-        if (!hr[s].pack.empty()) {
+        SETDEV(S);
+        if (!hr[s].pack.empty() && work(s, false, "halo_pack")) {
             hipLaunchKernelGGL(k_copy_runs, dim3((unsigned)std::min<size_t>(hr[s].pack.size(), 4096)), dim3(256), 0, S.s,
                                (const Run *)S.d_pack, (long)hr[s].pack.size(), (const u64 *)S.col[0].dig, S.hsend);
             MCHK(hipGetLastError());
         }
-        MCHK(hipEventRecord(S.ev, S.s));
+        if ((rc = rec(rk, s, EV_MAIN))) return rc;
     }
     for (int d = 0; d < p.world; ++d) {
         Rank &D = rk[d];
-        MCHK(hipSetDevice(D.dev));
+        SETDEV(D);
         for (int s = 0; s < p.world; ++s) {
             const Rank &S = rk[s];
             const long n = hr[s].send_cnt[d];
             if (!n) continue;
-            if (s != d) MCHK(hipStreamWaitEvent(D.s, S.ev, 0));
+            if (s != d && (rc = wait(rk, d, false, s, EV_MAIN))) return rc;
+            if (!copy_from(d, false, "halo", s)) continue;
             u64 *dp = hr[d].recv_halo[s] >= 0 ? D.halo + hr[d].recv_halo[s] : D.hstage + hr[d].recv_stage[s];
             const u64 *sp = S.hsend + hr[s].send_off[d];
             if (S.dev == D.dev) MCHK(hipMemcpyAsync(dp, sp, (size_t)n * 8, hipMemcpyDeviceToDevice, D.s));
             else MCHK(hipMemcpyPeerAsync(dp, D.dev, sp, S.dev, (size_t)n * 8, D.s));
         }
-        if (!hr[d].scatter.empty()) {
+        if (!hr[d].scatter.empty() && work(d, false, "halo_scatter")) {
             hipLaunchKernelGGL(k_copy_runs, dim3((unsigned)std::min<size_t>(hr[d].scatter.size(), 4096)), dim3(256), 0,
                                D.s, (const Run *)D.d_scatter, (long)hr[d].scatter.size(), (const u64 *)D.hstage, D.halo);
             MCHK(hipGetLastError());
         }
     }
     for (int d = 0; d < p.world; ++d) {
-        MCHK(hipSetDevice(rk[d].dev));
-        MCHK(hipEventRecord(rk[d].ev, rk[d].s));
+        SETDEV(rk[d]);
+        if ((rc = rec(rk, d, EV_MAIN))) return rc;
     }
     return MPFFT_OK;
 }
 
 // the whole multiply from every rank's operand slices (R.in) to its product stripes (R.out),
-// queued on the ranks' streams with no host synchronisation
+// queued on the ranks' streams with no host synchronisation.
+//
+// Event audit (tests/test_multi_schedule.py checks the recorded graph): an exchange's receivers
+// wait for the senders' events before any of them is recorded again (run_copies, run_halo,
+// run_exchange_fwd record in a separate loop or into a separate event); the stripe summaries are
+// published in their own event evs, so phase 1 of rank d waits for phase 0 of every rank, never
+// for another rank's phase 1; and a call starts, on every rank, after the end (evd) of every
+// other rank's previous call -- its first writes to rank e's arrays (the split into the column
+// arrays, exchange #1 into the row arrays) would otherwise overtake the previous call's pulls
+// from them on the other ranks' streams (exchange #2 from e's row arrays, the halo send block,
+// the summaries).
 int run_ranks(const Part &p, std::vector<Rank> &rk, const std::vector<HaloRank> &halo, unsigned long depth,
               unsigned long w)
 {
     int rc;
+    for (int d = 0; d < p.world; ++d) {
+        SETDEV(rk[d]);
+        for (int e = 0; e < p.world; ++e)
+            if (e != d && rk[e].done_rec && (rc = wait(rk, d, false, e, EV_DONE))) return rc;
+    }
     if (p.rep) {
         if ((rc = fwd_replicated(p, rk, depth, w))) return rc;
     } else {
@@ -649,33 +763,42 @@ int run_ranks(const Part &p, std::vector<Rank> &rk, const std::vector<HaloRank> 
     if ((rc = stage_all(p, rk, MPFFT_SHARD_INV_ROWS, depth, w))) return rc;
     std::vector<mpfft_copy> plan;
     exchange_plan(p, MPFFT_XCHG_ROW_TO_COL, plan);
-    if ((rc = run_copies(p, rk, plan))) return rc;
+    if ((rc = run_copies(p, rk, plan, "xchg2"))) return rc;
     if ((rc = stage_all(p, rk, MPFFT_SHARD_INV_COLUMNS, depth, w))) return rc;
     if ((rc = run_halo(p, rk, halo))) return rc;
     // combine phase 0: every stripe with carry-in 0 and its (generate, propagate) summary
     for (int d = 0; d < p.world; ++d) {
         Rank &R = rk[d];
-        MCHK(hipSetDevice(R.dev));
+        SETDEV(R);
         const mpfft_shard sh = desc(p, d, R, depth, w);
-        if ((rc = mpfft_shard_combine(&sh, 0, R.out, R.halo, R.sums, nullptr, R.tmp, R.tmp_bytes, R.s))) return rc;
-        MCHK(hipEventRecord(R.ev, R.s));
+        if (work(d, false, "combine0") &&
+            (rc = mpfft_shard_combine(&sh, 0, R.out, R.halo, R.sums, nullptr, R.tmp, R.tmp_bytes, R.s)))
+            return rc;
+        if ((rc = rec(rk, d, EV_SUM))) return rc;
     }
     // every rank's summaries to every rank (Tr pairs each), then phase 1: each rank scans the
-    // stripes below each of its own on the device and adds the carry
+    // stripes below each of its own on the device and adds the carry.  The pulls wait on evs
+    // (phase 0), which no rank re-records in this loop: phase 1 runs on all ranks at once
+    // (waiting on ev, re-recorded after each rank's phase 1 here, chained them 0 -> 1 -> ...)
     const size_t sb = (size_t)p.Tr * 2 * sizeof(int);
     for (int d = 0; d < p.world; ++d) {
         Rank &R = rk[d];
-        MCHK(hipSetDevice(R.dev));
+        SETDEV(R);
         for (int e = 0; e < p.world; ++e) {
             const Rank &E = rk[e];
-            if (e != d) MCHK(hipStreamWaitEvent(R.s, E.ev, 0));
+            if (e != d && (rc = wait(rk, d, false, e, EV_SUM))) return rc;
+            if (!copy_from(d, false, "sums", e)) continue;
             int *dp = R.sums_all + (size_t)e * p.Tr * 2;
             if (E.dev == R.dev) MCHK(hipMemcpyAsync(dp, E.sums, sb, hipMemcpyDeviceToDevice, R.s));
             else MCHK(hipMemcpyPeerAsync(dp, R.dev, E.sums, E.dev, sb, R.s));
         }
         const mpfft_shard sh = desc(p, d, R, depth, w);
-        if ((rc = mpfft_shard_combine(&sh, 1, R.out, R.halo, R.sums, R.sums_all, R.tmp, R.tmp_bytes, R.s))) return rc;
-        MCHK(hipEventRecord(R.ev, R.s));
+        if (work(d, false, "combine1") &&
+            (rc = mpfft_shard_combine(&sh, 1, R.out, R.halo, R.sums, R.sums_all, R.tmp, R.tmp_bytes, R.s)))
+            return rc;
+        if ((rc = rec(rk, d, EV_MAIN))) return rc;
+        if ((rc = rec(rk, d, EV_DONE))) return rc;
+        R.done_rec = true;
     }
     return MPFFT_OK;
 }
@@ -713,6 +836,16 @@ int prepare(Ctx &X, const Part &p, const std::vector<int> &devs, bool host)
         halo_xfer(p, X.halo);
         X.key = key;
     }
+    // a rank whose buffers grow frees its old allocation: other ranks' streams (other devices)
+    // may still be pulling from it -- exchange #2 from its row arrays, the halo send block, the
+    // summaries -- after the previous device-resident call, which returns without a host sync
+    bool grows = false;
+    for (int d = 0; d < p.world; ++d) {
+        size_t hb = 0;
+        const size_t need = rank_need(p, d, host, X.halo[d], &hb);
+        if (X.ranks[d].mem_bytes < need || X.ranks[d].host_bytes < hb) grows = true;
+    }
+    if (grows) drain(X.ranks);
     for (int d = 0; d < p.world; ++d) {
         int rc = setup_rank(p, d, X.ranks[d], host, X.halo[d]);
         if (rc) return rc;
@@ -1016,6 +1149,33 @@ int mpfft_multi_release(void)
     g_ctx.devs.clear();
     (void)hipSetDevice(cur);
     return MPFFT_OK;
+}
+
+long mpfft_multi_schedule(long n1, long n2, unsigned long depth, unsigned long w, int world, int calls, char *buf,
+                          size_t len)
+{
+    Part p;
+    int rc = partition(p, n1, n2, depth, w, world);
+    if (rc) return -rc;
+    if (calls < 1) return -MPFFT_EINVAL;
+    std::vector<Rank> rk(world);
+    std::vector<HaloRank> hr;
+    halo_xfer(p, hr);
+    Sched sc;
+    sc.dry = true;
+    g_sched = &sc;
+    for (int k = 0; k < calls && !rc; ++k) {
+        if (k) sched_line("N");
+        rc = run_ranks(p, rk, hr, depth, w);
+    }
+    g_sched = nullptr;
+    if (rc) return -rc;
+    if (buf && len) {
+        const size_t n = std::min(len - 1, sc.log.size());
+        memcpy(buf, sc.log.data(), n);
+        buf[n] = 0;
+    }
+    return (long)sc.log.size() + 1;
 }
 
 int mpfft_set_devices(int ngpus, const int *devices, long min_l)

@@ -667,14 +667,6 @@ __device__ __forceinline__ void rp_pin(Pr (&x)[G][R])
     RP_FENCE();
 }
 
-// slots of the fused split whose source limbs are in flight together (k_rpass MODE 2): 4 at
-// l <= 2048 (C3 forward columns 1.80 -> 1.78 ms, C2 1.42 -> 1.39 against one at a time), one at
-// l = 4096 (C4 19.72 vs 19.86 ms with 4); profiles/r05/split_batch_ab.txt.  A/B: -DRP_SPLIT_BATCH=n
-#ifndef RP_SPLIT_BATCH
-#define RP_SPLIT_BATCH 0
-#endif
-constexpr int rp_split_batch(int PP) { return RP_SPLIT_BATCH ? RP_SPLIT_BATCH : PP >= 4 ? 1 : 4; }
-
 // MODE: DIR 0: 0 plain, 1 MFA twiddle on load, 2 split on load (first column pass),
 //               3 plain with inputs that still owe an earlier pass's pending exponents
 //               (PassArgs::pcarry: applied by a rotated load, rp_load_limbs_rot, so the
@@ -769,45 +761,34 @@ __global__ __launch_bounds__(rp_nt(1024 * PP, LOGG, DIR), 4) void k_rpass(PassAr
         __syncthreads();
         rp_decode<G, G, PP, NT>(x, CODE, t);
     } else {   // first forward column pass: FFT_split_bits fused into the load
-        // the 3 source limbs per pair of RP_SPLIT_BATCH slots requested before any is used (clamped
-        // loads, src_limb_nb: one load round trip per batch, not per slot)
-        constexpr int SB = rp_split_batch(PP) < G ? rp_split_batch(PP) : G;
-        const SrcSlice sv{a.src_chunk, a.jNC, a.sub_off};
+        // one slot at a time, guarded loads (a zero slot, and the lanes past the coefficient's
+        // bits1 bits -- the upper half of every split coefficient -- issue none).  Round 5 put four
+        // slots' loads in flight from clamped addresses: C3's pass 0.735 -> 0.885 ms, C4's 5.17 ->
+        // 6.05 (every dead lane loaded); with wave-uniform skips of the dead waves and zero slots
+        // still 0.771 / 5.29 ms (profiles/r06/split_ab.txt), so this form stays
 #pragma unroll
-        for (int i0 = 0; i0 < G; i0 += SB) {
-            __builtin_amdgcn_sched_barrier(0);
-            u64 raw[SB][R][3];
+        for (int i = 0; i < G; ++i) {
+            __builtin_amdgcn_sched_barrier(0);   // 3 source limbs per pair, a slot at a time
+            const bool z = zero_in(i);
 #pragma unroll
-            for (int k = 0; k < SB; ++k) {
-                const int i = i0 + k;
+            for (int r = 0; r < R; ++r) {
+                const int pp = t + NT * r;
+                x[i][r] = Pr{{0, 0, 0, 0}, 0};
+                if (z) continue;
+                const u64 left = (u64)pp * 128 < a.bits1 ? a.bits1 - (u64)pp * 128 : 0;   // bits of the coefficient here
                 const long j = (long)(a.pos_off + g.pos0 + i * g.pstep) * a.jNC + a.sub_off + sub;
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const int pp = t + NT * r;
-                    const u64 off = (u64)j * a.bits1 + (u64)pp * 128;
-                    const long q = (long)(off >> 6);
-                    const bool live = !zero_in(i) && (u64)pp * 128 < a.bits1;   // bits of the coefficient here
-                    const long ns = live ? a.nsrc[op] : 0;
-#pragma unroll
-                    for (int m = 0; m < 3; ++m) raw[k][r][m] = src_limb_nb(src, ns, sv, j, a.bits1, q + m);
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < SB; ++k) {
-                const int i = i0 + k;
-                const long j = (long)(a.pos_off + g.pos0 + i * g.pstep) * a.jNC + a.sub_off + sub;
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const int pp = t + NT * r;
-                    const u64 left = (u64)pp * 128 < a.bits1 ? a.bits1 - (u64)pp * 128 : 0;
-                    const int sh = (int)(((u64)j * a.bits1 + (u64)pp * 128) & 63);
-                    const u64 x0 = raw[k][r][0], x1 = raw[k][r][1], x2 = raw[k][r][2];
-                    u64 f0 = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
-                    u64 f1 = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
-                    f0 = left < 64 ? f0 & ((((u64)1) << left) - 1) : f0;
-                    f1 = left <= 64 ? 0 : left < 128 ? f1 & ((((u64)1) << (left - 64)) - 1) : f1;
-                    x[i][r] = pr_make(rp_v4u{(u32)f0, (u32)(f0 >> 32), (u32)f1, (u32)(f1 >> 32)}, 0);
-                }
+                const u64 off = (u64)j * a.bits1 + (u64)pp * 128;
+                const long q = (long)(off >> 6);
+                const int sh = (int)(off & 63);
+                const long ns = left ? a.nsrc[op] : 0;
+                const SrcSlice sv{a.src_chunk, a.jNC, a.sub_off};
+                const u64 x0 = src_limb(src, ns, sv, j, a.bits1, q), x1 = src_limb(src, ns, sv, j, a.bits1, q + 1),
+                          x2 = src_limb(src, ns, sv, j, a.bits1, q + 2);
+                u64 f0 = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
+                u64 f1 = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
+                f0 = left < 64 ? f0 & ((((u64)1) << left) - 1) : f0;
+                f1 = left <= 64 ? 0 : left < 128 ? f1 & ((((u64)1) << (left - 64)) - 1) : f1;
+                x[i][r] = pr_make(rp_v4u{(u32)f0, (u32)(f0 >> 32), (u32)f1, (u32)(f1 >> 32)}, 0);
             }
         }
     }

@@ -83,6 +83,38 @@ def test_mul_multi_device_entry(mp, oracle, world, depth, w, n1, n2):
     assert (got == want).all()
 
 
+@pytest.mark.parametrize("world", [2, 8])
+def test_mul_multi_device_back_to_back_rank_streams(mp, oracle, world):
+    """Two device-resident calls queued back to back on separate per-rank streams with no host
+    synchronisation between them, each call with its own operands and stripes: the second call's
+    first writes into a rank's arrays must wait for the first call's pulls from them on the other
+    ranks' streams (the event graph is checked on the CPU in test_multi_schedule.py).
+    Both products exact."""
+    import torch
+    dev = torch.device("cuda:0")
+    depth, w, n1, n2 = 15, 4, 2000000, 1900000
+    part = mp.shard_partition(n1, n2, depth, w, world)
+    sts = [torch.cuda.Stream(dev) for _ in range(world)]
+    calls = []
+    for k in range(2):
+        a = mp.fill_random(n1, 0x700 + 16 * k + world)
+        b = mp.fill_random(n2, 0x800 + 16 * k + world)
+        src1 = [torch.from_numpy(mp.shard_pack(a, n1, n2, depth, w, world, g).view(np.int64)).to(dev)
+                for g in range(world)]
+        src2 = [torch.from_numpy(mp.shard_pack(b, n1, n2, depth, w, world, g).view(np.int64)).to(dev)
+                for g in range(world)]
+        outs = [torch.full((part["Tr"] * part["SL"],), -1, dtype=torch.int64, device=dev) for _ in range(world)]
+        calls.append((oracle.gmp_mul(a, b), src1, src2, outs))
+    torch.cuda.synchronize()
+    for want, src1, src2, outs in calls:
+        mp.mul_multi_device(n1, n2, depth, w, [0] * world, src1, src2, outs, streams=sts)
+    for s in sts:
+        s.synchronize()
+    for want, src1, src2, outs in calls:
+        got = mp.assemble_stripes(part, world, [o.cpu().numpy().view(np.uint64) for o in outs])
+        assert (got == want).all()
+
+
 def test_mul_multi_c4_world2_digest(mp):
     """C4 over two ranks on device 0 with the default (replicated) forward columns, against the
     GMP digest"""
