@@ -128,6 +128,22 @@ def cpu_baseline(a, b, depth, w, reps, warmup=1):
             "cpu_model": cpu_model(), "nproc": os.cpu_count()}, ref, g
 
 
+def cpu_ncore(cfg, procs):
+    """The host's multi-core capacity beside the 1-core contract number (VERDICT r5 #6,
+    BASELINE.md's optional nproc-way figure): oracle/ncore.py runs K = min(procs, allowed cores,
+    free RAM / 4 GB) concurrent independent CPU new_mpn_mul calls of the bench operands, one
+    process per core, then K concurrent GMP mpn_mul calls.  Run before this process touches the
+    GPU; the workers import no torch."""
+    depth, w, nl = CONFIGS[cfg]
+    cmd = [sys.executable, os.path.join(ROOT, "oracle", "ncore.py"), "--procs", str(procs), "--depth", str(depth),
+           "--w", str(w), "--n", str(nl), "--seed1", str(SEED1), "--seed2", str(SEED2)]
+    try:
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+        return json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    except Exception as e:   # reported, never fatal: the 1-core figure is the contract number
+        return {"error": repr(e)}
+
+
 VALU_PEAK = 1024 * 32 * 2.4e9   # int32 lane-ops/s: 256 CUs x 4 SIMD-32 x 2.4 GHz (MI355X_MICROARCH.md)
 
 
@@ -345,6 +361,8 @@ def main():
     ap.add_argument("--cpu-reps", type=int, default=5, help="timed oracle calls (median; after one warm-up)")
     ap.add_argument("--cpu-warmup", type=int, default=1, help="untimed oracle calls before the timed ones")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-procs", type=int, default=16,
+                    help="cpu_baseline.ncore: concurrent CPU multiplies (one process per core; 0: skip)")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--e2e-reps", type=int, default=2)
     ap.add_argument("--no-twin", action="store_true",
@@ -376,6 +394,12 @@ def main():
             print(json.dumps({"n_gpus": 1, "ranks_seen": 1, "dry_run": True}))
         return
 
+    # the multi-core CPU figure first: its worker processes start before anything touches the GPU
+    ncore = None
+    if int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_cpu_baseline and not args.mul6 \
+            and args.mode in (None, "single") and args.cpu_procs > 0:
+        ncore = cpu_ncore(args.config or "C3", args.cpu_procs)
+
     import torch
     import torch.distributed as dist
     import mpfft_loader
@@ -395,10 +419,20 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
+        # A failure on some ranks only (an OOM partway through the sharded run) would leave the
+        # others blocked inside an RCCL collective that the failed rank never joins, short of the
+        # gloo barrier below where rank 0 falls back to the C entry's line.  Bounded waits turn that
+        # into a symmetric failure: the RCCL group times out after 240 s and, with
+        # TORCH_NCCL_ASYNC_ERROR_HANDLING=2 (clean up, do not tear the process down), the blocked
+        # collective raises on those ranks too; the gloo group's barriers wait up to 900 s.  (The
+        # symmetric case is rehearsed with MPFFT_BENCH_FAIL_SHARDED=1; the asymmetric one needs
+        # distinct GPUs and has not run.)
+        import datetime
         if share:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=900))
         else:
-            dist.init_process_group("nccl", device_id=dev)
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
+            dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(seconds=240))
 
     if args.mul6:
         print(json.dumps(bench_mul6(args, mp, dev, args.config or "C3")))
@@ -420,7 +454,7 @@ def main():
             res, sharded_err = None, repr(e)
         # the other ranks wait on a host-side (gloo) barrier while rank 0 times the C entry on
         # their devices: an RCCL barrier would leave a kernel spinning on each of those GPUs
-        host_pg = dist.new_group(backend="gloo") if world > 1 else None
+        host_pg = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=900)) if world > 1 else None
         if world > 1:
             dist.barrier(group=host_pg)
         if rank == 0:
@@ -595,6 +629,7 @@ def main():
         res["c4_single"] = single_gpu_line(mp, dev, "C4", 3, 1, check=not args.no_check)
     if world == 1 and not args.no_cpu_baseline:
         cb, ref, g = cpu_baseline(a, b, depth, w, args.cpu_reps, args.cpu_warmup)
+        cb["ncore"] = ncore
         res["cpu_baseline"] = cb
         res["exact_vs_port"] = bool((got == ref).all())
         res["exact_vs_gmp"] = bool((got == g).all())

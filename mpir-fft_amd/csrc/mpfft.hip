@@ -29,6 +29,7 @@
 
 #include "kernels.hpp"
 #include "combine.hpp"
+#include "fold.hpp"
 #include "wdispatch.hpp"
 #include "bdispatch.hpp"
 #include "pdispatch.hpp"
@@ -89,6 +90,9 @@ struct Plan {
     // (Exec::zflags) -- no stage between that pass and the combine may use this region
     size_t off_digA, off_topA, off_cbA, off_digB, off_topB, off_cbB, off_flags, bytes;
     bool has_c;         // a third coefficient array C: the fused pointwise (k_pwss PAIR) writes there
+    int fold;           // f4 (fold.hpp): scaling in the last inverse row pass, reduced-form combine with
+                        // KM = fold coefficients per wave (0: k_rscale + k_combine1)
+    size_t off_meta;    // k_cmeta's per-coefficient A_k, B_k (fold plans)
     int fuse_rows;      // row DIF levels that run inside the pointwise: 1 (slot pairs), 2 (slot quads), 0
     size_t off_digC, off_topC, off_cbC;
 };
@@ -263,8 +267,31 @@ static int make_plan_split(Plan *p, long n1, long n2, unsigned long depth, unsig
         p->off_cbC = o; o += cbb;
     }
     p->off_flags = o; o += align_up((size_t)(p->total / 256 + 8) * 4, 256);   // k_combine1 blocks at V = 1
+    // f4 fold (fold.hpp) on the truncated register-pass plans: KM coefficients reach a wave's 512
+    // product limbs (windows shifted by up to one bit); MPFFT_FOLD=0 (diagnostics): k_rscale + k_combine1
+    {
+        static const bool no_fold = [] { const char *e = diag_env("MPFFT_FOLD"); return e && !strcmp(e, "0"); }();
+        const int km = (int)((p->N + 1 + 32767) / p->bits1 + 1);
+        p->fold = (p->rpass && !sqrt2 && p->Tr < p->NR && p->bits1 > 512 && km <= 4 && !no_fold) ? (km <= 3 ? 3 : 4) : 0;
+    }
+    p->off_meta = o; o += align_up((size_t)p->slots * 4, 256);
     p->bytes = o;
     return MPFFT_OK;
+}
+
+// rows of the truncated inverse column transform whose top-level doubling Exec::itft leaves to
+// the scaling (defer_double): IFFT_radix2_truncate's t <= h branch doubles outputs [0, t), the
+// t > h branch [t - h, h) (mul_fft.c:1733-1790)
+static void plan_dbl(const Plan &P, long *lo, long *hi)
+{
+    const long t = P.Tr, h = P.NR / 2;
+    *lo = *hi = 0;
+    if (t == P.NR) return;
+    if (t <= h) *hi = t;
+    else {
+        *lo = t - h;
+        *hi = h;
+    }
 }
 
 // The matrix split of the MFA is internal (no internal ABI): the reference takes
@@ -363,6 +390,7 @@ struct Exec {
     long zflags_n = 0;       // (u32 words), so combine_single needs no separate fill launch
     int in_rows = 0;         // non-zero: inputs live in column rows [0, in_rows) (default: the trunc rows)
     bool defer_double = false;   // itft's top-level doubling is left to scale() (rows [dbl_lo, dbl_hi): 2^-depth)
+    bool fold = false;           // f4 (P.fold): 2^-(depth+1) in the last inverse row pass, no scale(), combine_fold()
     bool fuse_row_last = false;  // the row DIF's last level runs inside the pointwise (k_pwss PAIR)
     // forward columns: only output rows [own_lo, own_hi) are wanted (own_hi > 0).  After the
     // first column pass a DIF splits into independent subtrees of positions; the later passes
@@ -916,6 +944,7 @@ struct Exec {
                 PassArgs b = row_args();
                 b.lvl0 = hi - kk;
                 b.tw_mode = (hi - kk == 0) ? 2 : 0;
+                if (fold && hi - kk == 0) b.scale_e = 2 * P.N - (u64)(P.depth + 1);   // the scaling rides in the un-twiddle
                 return b;
             };
             const int k = fit(split(hi, false, true), 1, mk);
@@ -1145,7 +1174,7 @@ struct Exec {
     // scaling by 2^-(depth+1); rows [dbl_lo, dbl_hi) by 2^-depth (itft's deferred doubling)
     int scale()
     {
-        if (P.fuse_scale) return MPFFT_OK;   // done by the last inverse column pass
+        if (P.fuse_scale || fold) return MPFFT_OK;   // done by the last inverse column / row pass
         const u64 e = 2 * P.N - (u64)(P.depth + 1);
         if (dbl_hi <= dbl_lo) return scale_rows(0, P.Tr, e);
         if (P.rpass) return scale_rows(0, P.Tr, e, dbl_lo, dbl_hi);   // one launch, two exponents
@@ -1233,6 +1262,38 @@ struct Exec {
                                : (k3w ? k_combine1<8, 3, true> : k_combine1<8, 4, true>);
         }
         hipLaunchKernelGGL(f, dim3((unsigned)nb), dim3(nt), 0, s, a, r, st, allp);   // st[nb]: the ticket counter
+        HIPCHK(hipGetLastError());
+        return MPFFT_OK;
+    }
+
+    // f4: the combine from the reduced form (fold.hpp): k_cmeta, then k_combine_red; rows
+    // [lo, hi) of the coefficients doubled
+    int combine_fold(u64 *r, unsigned char *ws, long lo, long hi)
+    {
+        FoldArgs a;
+        memset(&a, 0, sizeof(a));
+        a.dig = row.dig[0];
+        a.cb = row.cb[0];
+        a.top = row.top[0];
+        a.meta = (int *)(ws + P.off_meta);
+        a.l = (int)P.l;
+        a.cbw = cb_words((int)P.l);
+        a.N = P.N;
+        a.bits1 = P.bits1;
+        a.len = P.len;
+        a.total = P.total;
+        a.lbC = P.lbC;
+        a.dbl_lo = (int)lo;
+        a.dbl_hi = (int)hi;
+        a.inv_bits1 = 1.0 / (double)P.bits1;
+        constexpr int NT = 512;
+        a.bps = (P.total + 8 * NT - 1) / (8 * NT);
+        u32 *st = comb_flags(ws);
+        if (zflags != st) HIPCHK(hipMemsetAsync(st, 0, (size_t)(a.bps + 1) * 4, s));
+        hipLaunchKernelGGL(k_cmeta, dim3((unsigned)((P.len + 255) / 256)), dim3(256), 0, s, a);   // a lane per coefficient
+        HIPCHK(hipGetLastError());
+        void (*f)(FoldArgs, u64 *, u32 *) = P.fold == 3 ? k_combine_red<3, NT> : k_combine_red<4, NT>;
+        hipLaunchKernelGGL(f, dim3((unsigned)a.bps), dim3(NT), 0, s, a, r, st);
         HIPCHK(hipGetLastError());
         return MPFFT_OK;
     }
@@ -1404,6 +1465,7 @@ static int run_all(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, un
     X.zflags = X.comb_flags(ws);
     X.zflags_n = X.comb_flag_words(P, P.total);
     X.defer_double = true;   // itft + scale back to back
+    X.fold = P.fold != 0;    // f4: no scaling pass, the combine reads the reduced form
     X.fuse_row_last = true;  // last row level inside the pointwise (nested negacyclic sizes)
     ProfCall pc;
     int rc;
@@ -1432,7 +1494,7 @@ static int run_all(const Plan &P, u64 *d_r, const u64 *d_i1, const u64 *d_i2, un
     pc.mark(5, s);
     if ((rc = X.scale())) return rc;
     pc.mark(6, s);
-    rc = X.combine_single(d_r, ws);
+    rc = X.fold ? X.combine_fold(d_r, ws, X.dbl_lo, X.dbl_hi) : X.combine_single(d_r, ws);
     pc.mark(7, s);
     return rc;
 }
@@ -1466,8 +1528,11 @@ int mpfft_stage_kernels(long n1, long n2, unsigned long depth, unsigned long w, 
     else
         snprintf(pw, sizeof pw, "k_pointwise (VALU)");
     const char *pair = P.rpass ? "k_rpair" : P.wave ? "k_wpair" : "k_pairop";
-    const char *scale = P.fuse_scale ? "(fused into the last inverse column pass)" : P.rpass ? "k_rscale" : P.wave ? "k_wscale" : "k_scale";
-    snprintf(buf, len, "%s;%s;%s;%s;%s + %s;%s;%s", pass, rows, pw, pass, pass, pair, scale, "k_combine1");
+    const char *scale = P.fuse_scale ? "(fused into the last inverse column pass)"
+                        : P.fold ? "(folded: 2^-(depth+1) in the last inverse row pass)"
+                        : P.rpass ? "k_rscale" : P.wave ? "k_wscale" : "k_scale";
+    const char *comb = P.fold ? "k_cmeta + k_combine_red (reduced form)" : "k_combine1";
+    snprintf(buf, len, "%s;%s;%s;%s;%s + %s;%s;%s", pass, rows, pw, pass, pass, pair, scale, comb);
     return MPFFT_OK;
 }
 
@@ -1600,6 +1665,12 @@ int mpfft_stage(int stage, const uint64_t *d_i1, const uint64_t *d_i2, uint64_t 
     case MPFFT_STAGE_INV_COLUMNS: return X.itft(0, P.NR, P.Tr);
     case MPFFT_STAGE_SCALE: return X.scale();
     case MPFFT_STAGE_COMBINE: return X.combine_single(d_r, (unsigned char *)d_ws);
+    case MPFFT_STAGE_FOLD_COMBINE: {
+        if (!P.fold) return MPFFT_EUNSUPPORTED;
+        long lo, hi;
+        plan_dbl(P, &lo, &hi);
+        return X.combine_fold(d_r, (unsigned char *)d_ws, lo, hi);
+    }
     }
     return MPFFT_EINVAL;
 }

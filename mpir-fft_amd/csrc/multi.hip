@@ -565,10 +565,14 @@ int queue_copy(std::vector<Rank> &rk, const mpfft_copy &c, bool xs, const char *
 {
     const Rank &S = rk[c.src], &D = rk[c.dst];
     const size_t es = c.field == 2 ? 4 : 8;
+    if (dry()) {   // a dry run has no buffers
+        copy_from(c.dst, xs, what, c.src);
+        return MPFFT_OK;
+    }
     void *dp = loc(D, c.dst_layout, c.op, c.field, c.dst_off);
     const void *sp = loc(S, c.src_layout, c.op, c.field, c.src_off);
-    if (!dry() && dp == sp) return MPFFT_OK;   // world 1: the row layout is a view of the column layout
-    if (!copy_from(c.dst, xs, what, c.src)) return MPFFT_OK;
+    if (dp == sp) return MPFFT_OK;   // world 1: the row layout is a view of the column layout
+    copy_from(c.dst, xs, what, c.src);
     const hipStream_t st = xs ? D.xs : D.s;
     if (S.dev == D.dev) MCHK(hipMemcpyAsync(dp, sp, c.count * es, hipMemcpyDeviceToDevice, st));
     else MCHK(hipMemcpyPeerAsync(dp, D.dev, sp, S.dev, c.count * es, st));

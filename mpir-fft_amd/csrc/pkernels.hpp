@@ -92,6 +92,12 @@ __host__ __device__ constexpr int pw_pd() { return pw_wpe<M, LK>() == 4 ? (pw_ti
 
 // L + T 2^N' == (L - (T + 1)) - 2^N'  (mod p'): subtract D = T + 1; returns the new top
 // (-1 unless the subtraction left [0, 2^N'), which needs L < D or L - D >= 2^N').
+// PW_NORM_SPILL_ALL (test builds only, libmpfft_pwspill.so): every lane takes the device form's
+// rare branch below -- keeps its top -- so the readers' T_q != -1 path runs on every exchange
+// (tests/test_gpu_parity.py::test_pointwise_norm_spill_branch)
+#ifndef PW_NORM_SPILL_ALL
+#define PW_NORM_SPILL_ALL 0
+#endif
 template <int M>
 __host__ __device__ __forceinline__ int pw_norm(u64 (&L)[M], int T)
 {
@@ -104,7 +110,7 @@ __host__ __device__ __forceinline__ int pw_norm(u64 (&L)[M], int T)
     // loop and spill it there (C4 pointwise 34.9 -> 34.1 ms, C3 3.47 -> 3.43 ms)
     {
         const u32 w0 = (u32)L[0], n0 = w0 - (u32)D;
-        const bool spill = D > 0 ? w0 < (u32)D : (D < 0 ? n0 < (u32)(-D) : false);
+        const bool spill = PW_NORM_SPILL_ALL || (D > 0 ? w0 < (u32)D : (D < 0 ? n0 < (u32)(-D) : false));
         L[0] = (L[0] & ~0xffffffffull) | (spill ? w0 : n0);
         return spill ? T : -1;
     }
@@ -131,8 +137,9 @@ __host__ __device__ __forceinline__ int pw_norm(u64 (&L)[M], int T)
 //         w_i = Xw[(i - Yw) mod 2M], complemented when i < Yw (i in [-1, 2M));
 //   2^E' x_q == out + 1 - (1 + T_q) 2^E'   (rotation wraps negated; T_q 2^N' == -T_q);
 //   negated (E >= N', or the signs differ):  ~out + 1 + (1 + T_q) 2^E'.
-// After pw_norm T_q = -1, so the (1 + T_q) term is a rare branch, and the whole sum is
-// one add-with-carry chain with carry-in 1.
+// After pw_norm T_q = -1 on all but ~2^-32 of the lanes (a lane whose low word would under- or
+// overflow keeps its top, pw_norm's device form), so the (1 + T_q) term is a rare branch, and the
+// whole sum is one add-with-carry chain with carry-in 1.
 // packed: the partner's 2 T_q + S_q (TT[q], or a register in the tight form)
 // FIXE >= 0: the caller guarantees E mod N' == FIXE, so the rotation is a compile-time constant
 // and every wrap test, word address and complement mask below folds away (the forward

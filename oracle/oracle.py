@@ -12,7 +12,9 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB = os.path.join(_HERE, "liboracle.so")
+# MPFFT_ORACLE_LIB: another build of the same source (make -C oracle asan: AddressSanitizer +
+# UBSan, scripts/asan_cpu.sh)
+_LIB = os.environ.get("MPFFT_ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")
 _lib = None
 
 _u64p = ctypes.POINTER(ctypes.c_uint64)

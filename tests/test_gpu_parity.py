@@ -275,6 +275,42 @@ def test_nested_pointwise_full_products(mp, oracle):
             os.environ["MPFFT_POINTWISE"] = old
 
 
+def test_pointwise_norm_spill_branch(mp, oracle):
+    """k_pwss's rare pw_norm branch (a lane whose low word would under/overflow keeps its top,
+    ~2^-32 per lane, so random inputs never reach it) and the readers' T_q != -1 path behind it,
+    on every lane of every exchange: libmpfft_pwspill.so is the shipped build with pwss.hip
+    compiled -DPW_NORM_SPILL_ALL=1 (csrc/Makefile `pwspill`, built by build()).  Whole products
+    through its C ABI at l = 1024 (k_pwss forced), 2048 (C2's fused quad) and 4096 against GMP
+    (ADVICE r5)."""
+    import ctypes
+    path = os.path.join(os.path.dirname(mp.LIB_PATH), "libmpfft_pwspill.so")
+    assert os.path.exists(path), "build() builds libmpfft_pwspill.so"
+    v = ctypes.CDLL(path)
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    v.mpfft_mul_ex.argtypes = [u64p, u64p, ctypes.c_long, u64p, ctypes.c_long, ctypes.c_ulong, ctypes.c_ulong]
+    v.mpfft_mul_ex.restype = ctypes.c_int
+    p = lambda x: x.ctypes.data_as(u64p)
+    old = os.environ.get("MPFFT_POINTWISE")
+    os.environ["MPFFT_POINTWISE"] = "pwss"
+    try:
+        for depth, w, n1, n2 in ((6, 1024, 32760, 32000), (15, 4, 15625000, 15625000), (7, 2048, 150000, 120000),
+                                 (6, 4096, 131064, 100000)):
+            assert mp.stage_kernels(n1, n2, depth, w)["pointwise"].startswith("k_pwss<")
+            a = mp.fill_random(n1, 0x5005 + depth)
+            b = mp.fill_random(n2, 0x6006 + w)
+            r = np.zeros(n1 + n2, dtype=np.uint64)
+            assert v.mpfft_mul_ex(p(r), p(a), n1, p(b), n2, depth, w) == 0
+            assert (r == oracle.gmp_mul(a, b)).all(), (depth, w, n1, n2)
+            o1, o2 = np.full(n1, 2**64 - 1, dtype=np.uint64), np.full(n2, 2**64 - 1, dtype=np.uint64)
+            assert v.mpfft_mul_ex(p(r), p(o1), n1, p(o2), n2, depth, w) == 0
+            assert (r == oracle.gmp_mul(o1, o2)).all(), ("all ones", depth, w, n1, n2)
+    finally:
+        if old is None:
+            os.environ.pop("MPFFT_POINTWISE", None)
+        else:
+            os.environ["MPFFT_POINTWISE"] = old
+
+
 @pytest.mark.parametrize("depth,w,nl", [(13, 32, 9800000), (11, 128, 2600000), (7, 2048, 150000)])
 def test_fill_fold_l4096_case_b(mp, oracle, depth, w, nl):
     """The truncated inverse's FILL step folded into the last DIT pass of a block IFFT

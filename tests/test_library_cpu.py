@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def declared_functions():
     src = open(os.path.join(ROOT, "include", "mpfft.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:void|int|size_t|const char \*)\s*\*?\s*(\w+)\s*\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:void|int|long|size_t|const char \*)\s*\*?\s*(\w+)\s*\(", src, flags=re.M)))
 
 
 def test_exports_every_declared_symbol(mp):
@@ -131,3 +131,14 @@ def test_pwss_pair_order_is_a_permutation():
         where = {v: b for b, v in enumerate(s)}
         for p in range(0, nb - nb % 16, 2):
             assert where[p] % 8 == where[p + 1] % 8, (nb, p)
+
+
+def test_fold_plans_on_bench_configs(mp):
+    """C2, C3, C4 (truncated, l = 2048 / 4096) run without a scaling pass -- the
+    2^-(depth+1) in the last inverse row pass, the reduced-form combine (fold.hpp); C1 (l = 256,
+    wave kernels) and the sqrt2 front end keep k_rscale / k_wscale + k_combine1"""
+    for depth, w, n in ((15, 4, 15625000), (15, 4, 20312500), (17, 2, 156250000)):
+        k = mp.stage_kernels(n, n, depth, w)
+        assert "k_combine_red" in k["combine"] and "folded" in k["scale"], k
+    k = mp.stage_kernels(261952, 261952, 11, 8)
+    assert "k_combine_red" not in k["combine"] and "folded" not in k["scale"]
