@@ -92,6 +92,9 @@ struct Plan {
     bool has_c;         // a third coefficient array C: the fused pointwise (k_pwss PAIR) writes there
     int fold;           // f4 (fold.hpp): scaling in the last inverse row pass, reduced-form combine with
                         // KM = fold coefficients per wave (0: k_rscale + k_combine1)
+    bool ltw;           // fold plans: the inverse MFA twiddle and the scaling ride in the first pass of
+                        // each column block of the truncated inverse (k_rpass DIT mode bit 3) instead
+                        // of the rows' last pass (every block's rotation a whole number of limb pairs)
     size_t off_meta;    // k_cmeta's per-coefficient A_k, B_k (fold plans)
     int fuse_rows;      // row DIF levels that run inside the pointwise: 1 (slot pairs), 2 (slot quads), 0
     size_t off_digC, off_topC, off_cbC;
@@ -273,6 +276,11 @@ static int make_plan_split(Plan *p, long n1, long n2, unsigned long depth, unsig
         static const bool no_fold = [] { const char *e = diag_env("MPFFT_FOLD"); return e && !strcmp(e, "0"); }();
         const int km = (int)((p->N + 1 + 32767) / p->bits1 + 1);
         p->fold = (p->rpass && !sqrt2 && p->Tr < p->NR && p->bits1 > 512 && km <= 4 && !no_fold) ? (km <= 3 ? 3 : 4) : 0;
+        static const bool no_ltw = [] { const char *e = diag_env("MPFFT_LTW"); return e && !strcmp(e, "0"); }();
+        // where it measured faster: l <= 2048 (C3 inverse rows + columns 1.714 -> 1.679 ms); at
+        // l = 4096 the rotated loads in the three-level column passes cost more than the rows save
+        // (C4 15.54 -> 15.84 ms), profiles/r06/ltw_ab.txt
+        p->ltw = p->fold && ((u64)p->w * (u64)p->NC) % 128 == 0 && p->l <= 2048 && !no_ltw;
     }
     p->off_meta = o; o += align_up((size_t)p->slots * 4, 256);
     p->bytes = o;
@@ -519,9 +527,11 @@ struct Exec {
             return a.pcarry ? 3 : 0;
         }
         if (a.tw_mode == 1) return -1;
-        const int gx = (a.tw_mode == 2 || a.scale_e) ? 1 : 0;
+        const bool ltw = a.tw_mode == 3, hl = a.lvl0 + logg == a.lbM;   // 3: the inverse twiddle on load (it takes scale_e too)
+        if (ltw && !hl) return -1;
+        const int gx = !ltw && (a.tw_mode == 2 || a.scale_e) ? 1 : 0;
         if (a.fill_off && gx) return -1;
-        return gx | (a.lvl0 + logg == a.lbM ? 2 : 0) | (a.fill_off ? 4 : 0);
+        return gx | (hl ? 2 : 0) | (a.fill_off ? 4 : 0) | (ltw ? 8 : 0);
     }
 
     // the k_rpass mode pass() launches for these arguments, -1: another kernel family
@@ -943,8 +953,8 @@ struct Exec {
             auto mk = [&](int kk) {
                 PassArgs b = row_args();
                 b.lvl0 = hi - kk;
-                b.tw_mode = (hi - kk == 0) ? 2 : 0;
-                if (fold && hi - kk == 0) b.scale_e = 2 * P.N - (u64)(P.depth + 1);   // the scaling rides in the un-twiddle
+                b.tw_mode = (hi - kk == 0 && !(fold && P.ltw)) ? 2 : 0;   // (ltw: on load in the column blocks)
+                if (fold && !P.ltw && hi - kk == 0) b.scale_e = 2 * P.N - (u64)(P.depth + 1);   // the scaling rides in the un-twiddle
                 return b;
             };
             const int k = fit(split(hi, false, true), 1, mk);
@@ -974,6 +984,12 @@ struct Exec {
                 if (P.fuse_scale && hi - kk == 0 && m == P.NR) {   // the whole column inverse is this block
                     b.scale_e = 2 * P.N - (u64)(P.depth + 1);
                     b.canon = 1;
+                }
+                if (fold && P.ltw && hi == lbM) {   // the block's first pass: inverse MFA twiddle + scaling on load
+                    b.tw_mode = 3;
+                    b.tw_w = (u64)P.w;
+                    b.tw_lbR = P.lbR;
+                    b.scale_e = 2 * P.N - (u64)(P.depth + 1);
                 }
                 return b;
             };

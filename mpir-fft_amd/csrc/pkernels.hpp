@@ -526,6 +526,94 @@ __device__ __forceinline__ void pw_level(u64 (&L)[M], int &T, int &S, unsigned &
     if (cross) __syncthreads(); else pw_wave_sync();
 }
 
+// Two DIT levels per exchange (A/B builds: -DPW_R4_INV=1): levels jj (pairs h1 =
+// K >> (lk - jj)) and jj + 1 (h2 = 2 h1) on the quad t0 | {0, h1, h2, h1 + h2} of role i = [t & h1]
+// + 2 [t & h2], from one publish: with A, B_i the two levels' twiddles (B_i that of the level-(jj+1)
+// pair holding t) every output is v_i = sum_r sigma_ir w^-e_ir Z_r, e_i0 = 0, e_i1 = A, e_i2 = B_i,
+// e_i3 = A + B_i, sigma_i1 = -[i odd], sigma_i2 = -[i >= 2], sigma_i3 = sigma_i1 sigma_i2 -- own term
+// plus three rotated partner reads (pw_combine), one barrier pair instead of two.  Same LDS traffic
+// (one 2M-word publish + three reads against two + two), 1.5x the add chains.
+#ifndef PW_R4_INV
+#define PW_R4_INV 0
+#endif
+template <int M, int LK>
+__device__ __forceinline__ void pw_level4_dit(u64 (&L)[M], int &T, int &S, unsigned &P, u32 *Xw, int *TT, unsigned *PP,
+                                              unsigned W2, int t, int jj)
+{
+    constexpr int K = 1 << LK;
+    constexpr unsigned NP = 64 * M, N2 = 2 * NP;
+    static_assert(!pw_tight(K), "the radix-4 levels use the TT / PP arrays");
+    const int jA = LK - 1 - jj, jB = jA - 1;
+    const int h1 = K >> (jA + 1), h2 = 2 * h1;
+    const int role = ((t & h1) ? 1 : 0) | ((t & h2) ? 2 : 0);
+    const int t0 = t & ~(h1 | h2);
+    const unsigned A = (unsigned)((t & (h1 - 1)) << jA) * W2;   // < N' (as pw_level's tw)
+    const unsigned B = (unsigned)((t & (h2 - 1)) << jB) * W2;
+    const bool cross = h2 >= 64;
+    pw_publish<M, LK>(L, T, S, Xw, TT, t);
+    PP[t] = P;
+    if (cross) __syncthreads(); else pw_wave_sync();
+    const unsigned eA = A ? N2 - A : 0u, eB = B ? N2 - B : 0u;
+    auto ex = [&](int r) -> unsigned { return r == 0 ? 0u : r == 1 ? eA : r == 2 ? eB : pw_mod(eA + eB, N2); };
+    const bool n1 = role & 1, n2 = (role >> 1) & 1;
+    auto neg = [&](int r) -> bool { return r == 0 ? false : r == 1 ? n1 : r == 2 ? n2 : n1 != n2; };
+    const unsigned Pn = pw_mod(P + ex(role), N2);
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+        const int r = role ^ k;
+        const int q = t0 | ((r & 1) ? h1 : 0) | ((r & 2) ? h2 : 0);
+        const unsigned Pq = PP[q];
+        const int packed = TT[q];
+        unsigned E = pw_mod(Pq + ex(r) + 2 * N2 - Pn, N2);
+        if (neg(r)) E = pw_mod(E + NP, N2);
+        pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, k == 1 ? (neg(role) ? -1 : 1) : 1, Xw, packed, q, E);
+    }
+    P = Pn;
+    if (cross) __syncthreads(); else pw_wave_sync();
+}
+
+// The same for two DIF levels (A/B builds: -DPW_R4_FWD=1): levels jj (h1 = K >> (jj + 1)) and
+// jj + 1 (h2 = h1 / 2), role i = [t & h2] + 2 [t & h1]; with a_r = ((t0 | [r odd] h2) mod h1) 2^jj W2
+// and B = (t0 mod h2) 2^(jj+1) W2, v_i = sum_r (-1)^popcount(i & r) w^e_ir X_r,
+// e_ir = [i odd] B + [i >= 2] a_r.
+#ifndef PW_R4_FWD
+#define PW_R4_FWD 0
+#endif
+template <int M, int LK>
+__device__ __forceinline__ void pw_level4_dif(u64 (&L)[M], int &T, int &S, unsigned &P, u32 *Xw, int *TT, unsigned *PP,
+                                              unsigned W2, int t, int jj)
+{
+    constexpr int K = 1 << LK;
+    constexpr unsigned NP = 64 * M, N2 = 2 * NP;
+    static_assert(!pw_tight(K), "the radix-4 levels use the TT / PP arrays");
+    const int h1 = K >> (jj + 1), h2 = h1 / 2;
+    const int role = ((t & h2) ? 1 : 0) | ((t & h1) ? 2 : 0);
+    const int t0 = t & ~(h1 | h2);
+    const unsigned a0 = (unsigned)((t0 & (h1 - 1)) << jj) * W2, a1 = (unsigned)(((t0 | h2) & (h1 - 1)) << jj) * W2;
+    const unsigned B = (unsigned)((t0 & (h2 - 1)) << (jj + 1)) * W2;
+    const bool cross = h1 >= 64;
+    pw_publish<M, LK>(L, T, S, Xw, TT, t);
+    PP[t] = P;
+    if (cross) __syncthreads(); else pw_wave_sync();
+    auto ex = [&](int i, int r) -> unsigned {
+        return pw_mod(((i & 1) ? B : 0u) + ((i & 2) ? ((r & 1) ? a1 : a0) : 0u), N2);
+    };
+    auto neg = [&](int i, int r) -> bool { return __builtin_popcount(i & r) & 1; };
+    const unsigned Pn = pw_mod(P + ex(role, role), N2);
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+        const int r = role ^ k;
+        const int q = t0 | ((r & 1) ? h2 : 0) | ((r & 2) ? h1 : 0);
+        const unsigned Pq = PP[q];
+        const int packed = TT[q];
+        unsigned E = pw_mod(Pq + ex(role, r) + 2 * N2 - Pn, N2);
+        if (neg(role, r)) E = pw_mod(E + NP, N2);
+        pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, k == 1 ? (neg(role, role) ? -1 : 1) : 1, Xw, packed, q, E);
+    }
+    P = Pn;
+    if (cross) __syncthreads(); else pw_wave_sync();
+}
+
 // the highest compile-time-rotation level of operand B's transform in the late-B (l = 4096) form:
 // level 0 only -- while B transforms, A's transformed limbs are live, and the switch copies of
 // levels 1 and 2 pushed the kernel into spilling (96 -> 40 B per lane; C4 pointwise 34.0 -> 32.3 ms,
@@ -558,6 +646,12 @@ __device__ __forceinline__ void pw_transform(u64 (&L)[M], int &T, int &S, unsign
         if constexpr (LK >= 8 && FIXMAX >= 1) pw_level<M, LK, DIR, 1>(L, T, S, P, Xw, TT, PP, W2, t, 1);   // h = K/4 >= 64
         if constexpr (LK >= 9 && FIXMAX >= 2) pw_level<M, LK, DIR, 2>(L, T, S, P, Xw, TT, PP, W2, t, 2);   // h = K/8 >= 64
         jj = LK >= 9 && FIXMAX >= 2 ? 3 : LK >= 8 && FIXMAX >= 1 ? 2 : 1;
+    }
+    if constexpr (DIR == 1 && PW_R4_INV && !pw_tight(1 << LK)) {
+        for (; jj + 1 < LK; jj += 2) pw_level4_dit<M, LK>(L, T, S, P, Xw, TT, PP, W2, t, jj);
+    }
+    if constexpr (DIR == 0 && PW_R4_FWD && !pw_tight(1 << LK)) {
+        for (; jj + 1 < LK; jj += 2) pw_level4_dif<M, LK>(L, T, S, P, Xw, TT, PP, W2, t, jj);
     }
     for (; jj < LK; ++jj) pw_level<M, LK, DIR, -1>(L, T, S, P, Xw, TT, PP, W2, t, jj);
 }

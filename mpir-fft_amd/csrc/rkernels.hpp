@@ -403,6 +403,11 @@ __device__ __forceinline__ u32 rp_exp_entry(const PassArgs &a0, const BGeo &g, i
     if (CIN) a.pcarry = 0;
     if (e < G) {
         if (CIN) return rp_pend_pos((u32)a0.rho, a0.lbM, a0.lvl0 - a0.pcarry, a0.lvl0, (u32)(g.pos0 + e * g.pstep), N2);
+        if (DIR == 1 && a.tw_mode == 3) {   // the inverse MFA twiddle (and the scaling) on load, rows of a column block
+            const long row = (long)a.pos_off + g.pos0 + (long)e * g.pstep;
+            const u64 t = bp_mod2n(g.tw0 * (u64)revbin_dev(row, a.tw_lbR), N2);
+            return (u32)bp_mod2n((t ? N2 - t : 0) + a.scale_e, N2);
+        }
         if (!GX) return 0;
         return DIR == 0 ? (u32)bp_mod2n(g.tw0 + (u64)e * g.twst + cadd, N2) : (u32)bp_post(a, g, e, N2);
     }
@@ -673,7 +678,9 @@ __device__ __forceinline__ void rp_pin(Pr (&x)[G][R])
 //               first level still runs in registers);
 //       DIR 1: bit 0 general final multipliers (inverse twiddle / scaling), bit 1 the pass
 //               holds the transform's last DIT level (h = 1: its first level needs no rotation),
-//               bit 2 the truncated inverse's FILL step (PassArgs::fill_*; not with bit 0)
+//               bit 2 the truncated inverse's FILL step (PassArgs::fill_*; not with bit 0),
+//               bit 3 the inverse MFA twiddle and the scaling applied on load (PassArgs::tw_mode
+//               3: the first pass of a column block, the rows' last pass then plain -- fold plans)
 // (compile-time, so the register-only level and the LDS level are never both in one kernel:
 // a runtime choice between them spilled)
 template <int LOGG, int PP, int DIR, int MODE>
@@ -682,7 +689,7 @@ __global__ __launch_bounds__(rp_nt(1024 * PP, LOGG, DIR), 4) void k_rpass(PassAr
     constexpr int NT = rp_nt(1024 * PP, LOGG, DIR), R = rp_r(PP, NT);
     constexpr bool GX = DIR == 0 ? MODE == 1 : (MODE & 1) != 0, SPLIT = DIR == 0 && MODE == 2,
                    CIN = DIR == 0 && MODE == 3, HL = DIR == 1 && (MODE & 2) != 0,
-                   FILL = DIR == 1 && (MODE & 4) != 0;
+                   FILL = DIR == 1 && (MODE & 4) != 0, LTW = DIR == 1 && (MODE & 8) != 0;
     pass_clear_flags(a);
     constexpr int G = 1 << LOGG, NX = G / 2 > 2 ? G / 2 : 2;
     constexpr int l = 1024 * PP, HP = l / 2, cbw = 2 * l / 64;
@@ -708,8 +715,8 @@ __global__ __launch_bounds__(rp_nt(1024 * PP, LOGG, DIR), 4) void k_rpass(PassAr
     g.pos0 = bstart | lo;
     g.pstep = 1 << lobits;
     g.sbase = (long)sub * a.sub_stride;
-    const u64 rsub = a.tw_mode ? (u64)revbin_dev(a.sub_off + sub, a.tw_lbR) : 0;
-    g.tw0 = a.tw_w * (u64)(a.pos_off + g.pos0) * rsub;
+    const u64 rsub = a.tw_mode && a.tw_mode != 3 ? (u64)revbin_dev(a.sub_off + sub, a.tw_lbR) : 0;
+    g.tw0 = a.tw_mode == 3 ? a.tw_w * (u64)(a.sub_off + sub) : a.tw_w * (u64)(a.pos_off + g.pos0) * rsub;   // 3: the column
     g.twst = a.tw_w * (u64)g.pstep * rsub;
     auto slot_lane = [&](int i) -> long {   // any i (the code staging has two slots per wave)
         const int ps = a.pos_off + g.pos0 + i * g.pstep;
@@ -736,7 +743,7 @@ __global__ __launch_bounds__(rp_nt(1024 * PP, LOGG, DIR), 4) void k_rpass(PassAr
     unsigned short *CODE = (unsigned short *)smem;   // G HP codes (over the exchange slots)
     Pr x[G][R];
     u32 *EDGE = SLT + G;   // rp_shift_all's lane-63 table (rp_lds)
-    if (DIR == 0 && GX && RP_GX_LOAD) {   // MFA twiddle 2^(tw0 + s twst) of slot s (README:89), so every level is pair-aligned:
+    if ((DIR == 0 && GX && RP_GX_LOAD) || LTW) {   // MFA twiddle 2^(tw0 + s twst) of slot s (README:89), so every level is pair-aligned:
         // whole pairs by the rotated load, the rest by neighbour pairs in registers
         auto ef = [&](int i) -> u32 { return rp_uniform(EXPT[i]); };
         const RpCodes cd = rp_codes_load<G, PP>(st, SLT, t);

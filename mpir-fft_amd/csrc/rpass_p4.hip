@@ -3,13 +3,13 @@
 
 rp_fn rp_get_p4(int logg, int dir, int mode)
 {
-    static const rp_fn tab[2][8][4] = {
+    static const rp_fn tab[2][16][4] = {
         {
             {nullptr, k_rpass<1, 4, 0, 0>, k_rpass<2, 4, 0, 0>, k_rpass<3, 4, 0, 0>},
             {nullptr, k_rpass<1, 4, 0, 1>, k_rpass<2, 4, 0, 1>, k_rpass<3, 4, 0, 1>},
             {nullptr, k_rpass<1, 4, 0, 2>, k_rpass<2, 4, 0, 2>, k_rpass<3, 4, 0, 2>},
             {nullptr, k_rpass<1, 4, 0, 3>, k_rpass<2, 4, 0, 3>, k_rpass<3, 4, 0, 3>},
-            {}, {}, {}, {},
+            {}, {}, {}, {}, {}, {}, {}, {}, {}, {}, {}, {},
         },
         {
             {nullptr, k_rpass<1, 4, 1, 0>, k_rpass<2, 4, 1, 0>, k_rpass<3, 4, 1, 0>},
@@ -20,9 +20,17 @@ rp_fn rp_get_p4(int logg, int dir, int mode)
             {nullptr, nullptr, nullptr, nullptr},
             {nullptr, k_rpass<1, 4, 1, 6>, k_rpass<2, 4, 1, 6>, k_rpass<3, 4, 1, 6>},
             {nullptr, nullptr, nullptr, nullptr},
+            {nullptr, nullptr, nullptr, nullptr},
+            {nullptr, nullptr, nullptr, nullptr},
+            {nullptr, k_rpass<1, 4, 1, 10>, k_rpass<2, 4, 1, 10>, k_rpass<3, 4, 1, 10>},
+            {nullptr, nullptr, nullptr, nullptr},
+            {nullptr, nullptr, nullptr, nullptr},
+            {nullptr, nullptr, nullptr, nullptr},
+            {nullptr, k_rpass<1, 4, 1, 14>, k_rpass<2, 4, 1, 14>, k_rpass<3, 4, 1, 14>},
+            {nullptr, nullptr, nullptr, nullptr},
         },
     };
-    if (logg < 1 || logg > 3 || dir < 0 || dir > 1 || mode < 0 || mode > 7) return nullptr;
+    if (logg < 1 || logg > 3 || dir < 0 || dir > 1 || mode < 0 || mode > 15) return nullptr;
     return tab[dir][mode][logg];
 }
 
