@@ -112,21 +112,41 @@ __device__ int cmeta_full(const FoldArgs &a, long k, int lane)
     const int cl = (int)((cb[2 * (bl >> 6)] >> (bl & 63)) & 1) - (int)((cb[2 * (bl >> 6) + 1] >> (bl & 63)) & 1);
     const int T0 = a.top[k] + cl;
     const int i0 = lane * nl;
-    auto limb = [&](int i, u64 &u) -> int {   // limb i with its carry-in (mask bit i - 1); returns its local carry
-        const u64 x = d[i];
-        int c = 0;
-        if (i) {
-            const int b = i - 1;
-            c = (int)((cb[2 * (b >> 6)] >> (b & 63)) & 1) - (int)((cb[2 * (b >> 6) + 1] >> (b & 63)) & 1);
+    // the lane's limbs 8 at a time (16-B loads, all in flight), with their carry-ins: mask bits
+    // i - 1 (the lane's limbs lie in one 64-limb mask row; limb i0's carry-in is bit 63 of the
+    // row below)
+    const int W = i0 >> 6;
+    const cb_v2u mrow = *(const cb_v2u *)(cb + 2 * W);
+    const cb_v2u mprev = W ? *(const cb_v2u *)(cb + 2 * W - 2) : cb_v2u{0, 0};
+    auto cin_of = [&](int i) -> int {
+        if (i == 0) return 0;
+        const int b = i - 1;
+        const cb_v2u m = (b >> 6) == W ? mrow : mprev;
+        return (int)((m.x >> (b & 63)) & 1) - (int)((m.y >> (b & 63)) & 1);
+    };
+    auto batch = [&](int i, u64 (&x)[8]) {
+#pragma unroll
+        for (int q = 0; q < 8; q += 2) {
+            const cb_v2u v = *(const cb_v2u *)(d + i + q);
+            x[q] = v.x;
+            x[q + 1] = v.y;
         }
+    };
+    auto limb = [&](int i, u64 x, u64 &u) -> int {   // limb i with its carry-in; returns its local carry
+        const int c = cin_of(i);
         u = x + (u64)(i64)c;
         return (c == 1 && x == MPF_MAXL) ? 1 : (c == -1 && x == 0) ? -1 : 0;
     };
     u32 F = CF_ID;
-    for (int i = i0; i < i0 + nl; ++i) {
-        u64 u;
-        const int g = limb(i, u);
-        F = cf_then(F, cf_make(g, u));
+    for (int i = i0; i < i0 + nl; i += 8) {
+        u64 x[8];
+        batch(i, x);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            u64 u;
+            const int g = limb(i + q, x[q], u);
+            F = cf_then(F, cf_make(g, u));
+        }
     }
     const u32 I = cf_wave_scan(F, lane);
     u32 E = (u32)__shfl_up((int)I, 1);
@@ -134,19 +154,24 @@ __device__ int cmeta_full(const FoldArgs &a, long k, int lane)
     int c = cf_apply(E, 0);   // carry into limb i0 (none into limb 0)
     bool allz = true, allo = true;
     u64 Rfirst = 0, R = 0, prev = 0;
-    for (int i = i0; i < i0 + nl; ++i) {
-        u64 u;
-        const int g = limb(i, u);
-        R = u + (u64)(i64)c;
-        c = cf_apply(cf_make(g, u), c);
-        if (i == i0) {
-            Rfirst = R;
-        } else {
-            const u64 X = s ? (R << 1) | (prev >> 63) : R;   // Xlo's limb i (i >= 1)
-            allz = allz && X == 0;
-            allo = allo && X == MPF_MAXL;
+    for (int i = i0; i < i0 + nl; i += 8) {
+        u64 x[8];
+        batch(i, x);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            u64 u;
+            const int g = limb(i + q, x[q], u);
+            R = u + (u64)(i64)c;
+            c = cf_apply(cf_make(g, u), c);
+            if (i + q == i0) {
+                Rfirst = R;
+            } else {
+                const u64 X = s ? (R << 1) | (prev >> 63) : R;   // Xlo's limb i + q (>= 1)
+                allz = allz && X == 0;
+                allo = allo && X == MPF_MAXL;
+            }
+            prev = R;
         }
-        prev = R;
     }
     u64 pl = __shfl_up(R, 1);   // the limb below i0
     if (lane == 0) pl = 0;
@@ -398,32 +423,44 @@ __device__ __forceinline__ void fold_thread8(const FoldArgs &a, long mW, long mA
             const int sh = (int)(e0 & 63);
             const u64 pbits = sh ? (m0.x >> sh) | (m1.x << (64 - sh)) : m0.x;
             const u64 nbits = sh ? (m0.y >> sh) | (m1.y << (64 - sh)) : m0.y;
-            u32 vm = 0;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) vm |= (e0 + i >= 0 && e0 + i <= a.l - 2) ? 1u << i : 0u;
+            // bits e0 + i valid for 0 <= e0 + i <= l - 2
+            const long lb = e0 < 0 ? -e0 : 0, ub = (long)a.l - 1 - e0;
+            const u32 vm = (lb >= 8 || ub <= 0) ? 0u : ((ub >= 8 ? 0xffu : (1u << ub) - 1u) & ~((1u << lb) - 1u));
             cb = ((u32)pbits & vm) | (((u32)nbits & vm) << 8);
         }
-        if (cb) {
+        if (__ballot(cb != 0)) {   // branch-free per limb: d 2^shc with d in {-1, 0, 1} (shc wave-uniform)
             const int shc = (64 - r) & 63;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const int dd = (int)((cb >> i) & 1) - (int)((cb >> (8 + i)) & 1);
-                if (dd) acc_signed(lo[i], hi[i], dd, shc);
+                u64 t;
+                const bool c = add_ovf(lo[i], (u64)(i64)dd << shc, &t);
+                lo[i] = t;
+                hi[i] += (u32)((c ? 1 : 0) - (dd < 0 ? 1 : 0));
             }
         }
+        // A_k 2^N and B_k: each lands in one lane of the waves it reaches -- the 128-bit value
+        // formed once, added to the limb it names by selects
         const int vB = meta_B(mt[j]), vA = meta_A(mt[j]);
-        if (vB && kb >= PL && kb < PL + 512) {
-            const int bb = (int)(kb - PL), li = bb >> 6;
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-                if (i == li) acc_signed(lo[i], hi[i], vB, bb & 63);
-        }
         const u64 ka = kb + a.N;
-        if (vA && ka >= PL && ka < PL + 512) {
-            const int bb = (int)(ka - PL), li = bb >> 6;
+        const bool inB = vB && kb >= PL && kb < PL + 512, inA = vA && ka >= PL && ka < PL + 512;
+        if (__ballot(inB || inA)) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
-                if (i == li) acc_signed(lo[i], hi[i], vA, bb & 63);
+            for (int e = 0; e < 2; ++e) {
+                const bool in = e ? inA : inB;
+                const i64 x = in ? (e ? vA : vB) : 0;
+                const int bb = in ? (int)((e ? ka : kb) - PL) : 0, li = bb >> 6, b = bb & 63;
+                const u64 xl = (u64)x << b;
+                const u32 xh = (u32)(b ? (x >> (64 - b)) : (x < 0 ? -1 : 0));
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const bool m = i == li;
+                    u64 t;
+                    const bool c = add_ovf(lo[i], m ? xl : 0, &t);
+                    lo[i] = t;
+                    hi[i] += (m ? xh : 0u) + (c ? 1u : 0u);
+                }
+            }
         }
     }
 }
@@ -534,7 +571,8 @@ __global__ __launch_bounds__(NT, KM <= 3 ? 2048 / NT : 1) void k_combine_red(Fol
 #pragma unroll
     for (int k = 0; k < V; ++k) {
         Lx[t * V + k] = u[k] + (u64)(i64)c;
-        c = cf_apply(fk(k), c);
+        const int gq = (int)((gk >> (2 * k)) & 3u) - 1;   // 2: past the end (transparent)
+        c = gq == 2 ? c : gq + (c == 1 && u[k] == MPF_MAXL) - (c == -1 && u[k] == 0);
     }
     __syncthreads();
 #pragma unroll
