@@ -440,26 +440,24 @@ __device__ __forceinline__ void fold_thread8(const FoldArgs &a, long mW, long mA
             }
         }
         // A_k 2^N and B_k: each lands in one lane of the waves it reaches -- the 128-bit value
-        // formed once, added to the limb it names by selects
+        // formed once, added to the limb it names by selects.  Bits k bits1 and k bits1 + N are N
+        // (> a wave's 512 limbs) apart, so a wave holds at most one of the two: one select pass
         const int vB = meta_B(mt[j]), vA = meta_A(mt[j]);
         const u64 ka = kb + a.N;
         const bool inB = vB && kb >= PL && kb < PL + 512, inA = vA && ka >= PL && ka < PL + 512;
         if (__ballot(inB || inA)) {
+            const bool in = inB || inA;
+            const i64 x = inB ? vB : inA ? vA : 0;
+            const int bb = in ? (int)((inB ? kb : ka) - PL) : 0, li = bb >> 6, b = bb & 63;
+            const u64 xl = (u64)x << b;
+            const u32 xh = (u32)(b ? (x >> (64 - b)) : (x < 0 ? -1 : 0));
 #pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const bool in = e ? inA : inB;
-                const i64 x = in ? (e ? vA : vB) : 0;
-                const int bb = in ? (int)((e ? ka : kb) - PL) : 0, li = bb >> 6, b = bb & 63;
-                const u64 xl = (u64)x << b;
-                const u32 xh = (u32)(b ? (x >> (64 - b)) : (x < 0 ? -1 : 0));
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const bool m = i == li;
-                    u64 t;
-                    const bool c = add_ovf(lo[i], m ? xl : 0, &t);
-                    lo[i] = t;
-                    hi[i] += (m ? xh : 0u) + (c ? 1u : 0u);
-                }
+            for (int i = 0; i < 8; ++i) {
+                const bool m = i == li;
+                u64 t;
+                const bool c = add_ovf(lo[i], m ? xl : 0, &t);
+                lo[i] = t;
+                hi[i] += (m ? xh : 0u) + (c ? 1u : 0u);
             }
         }
     }

@@ -458,6 +458,9 @@ __device__ __forceinline__ void pw_combine_fixed(u64 (&L)[M], int &T, int &S, in
     }
 }
 
+#ifndef PW_PROBE_NOH1
+#define PW_PROBE_NOH1 0   // 1: timing probe, the h = 1 levels without their LDS round (A/B builds only)
+#endif
 // one level jj of the transform.  FIXJ >= 0 (forward transforms, level jj = FIXJ): E mod N' is
 // wave-uniform and one of 2^FIXJ compile-time values (level 0: exactly N'/2) -- pw_transform
 template <int M, int LK, int DIR, int FIXJ>
@@ -474,6 +477,19 @@ __device__ __forceinline__ void pw_level(u64 (&L)[M], int &T, int &S, unsigned &
     // (qt mod h) 2^j < K/2, times W2: below N' (= K W2 / 2): no reduction needed
     const unsigned tw = (unsigned)((qt & (h - 1)) << j) * W2;
     const bool cross = h >= 64;                  // partner in another wave
+#if PW_PROBE_NOH1
+    if (h == 1) {   // timing probe (A/B builds only, wrong products): the h = 1 level without its LDS round
+        u64 cy = P;
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const u64 s = L[m] + cy;
+            cy = s < L[m] ? 1 : 0;
+            L[m] = s;
+        }
+        if (!top) P = pw_mod(P + 1, N2);
+        return;
+    }
+#endif
     unsigned Pq;
     int packed;
     if (pw_tight(K)) {

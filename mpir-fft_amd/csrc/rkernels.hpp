@@ -268,6 +268,15 @@ __device__ __forceinline__ Pr rp_get_rot(const RX<PP> &X, int j, int pp, u32 e, 
 #ifndef RP_GX_LOAD
 #define RP_GX_LOAD 1   // 0: the round-3 form (plain load, general rotation through LDS), A/B builds only
 #endif
+#ifndef RP_SPLIT_ZSKIP
+#define RP_SPLIT_ZSKIP 1   // 0 (A/B builds): the split pass exchanges its zero slots like any other
+#endif
+#ifndef RP_SPLIT_LDS
+#define RP_SPLIT_LDS 1     // 0 (A/B builds): the split pass's per-slot guarded loads for whole operands too
+#endif
+#ifndef RP_SPLIT_PROBE
+#define RP_SPLIT_PROBE 0   // 1: timing probe, the split pass's source loads replaced by arithmetic (A/B builds only)
+#endif
 __device__ __forceinline__ u32 rp_ror1(u32 v) { return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x13C, 0xF, 0xF, false); }
 
 template <int G, int PP, int NT, typename EF>
@@ -768,34 +777,94 @@ __global__ __launch_bounds__(rp_nt(1024 * PP, LOGG, DIR), 4) void k_rpass(PassAr
         __syncthreads();
         rp_decode<G, G, PP, NT>(x, CODE, t);
     } else {   // first forward column pass: FFT_split_bits fused into the load
-        // one slot at a time, guarded loads (a zero slot, and the lanes past the coefficient's
-        // bits1 bits -- the upper half of every split coefficient -- issue none).  Round 5 put four
-        // slots' loads in flight from clamped addresses: C3's pass 0.735 -> 0.885 ms, C4's 5.17 ->
-        // 6.05 (every dead lane loaded); with wave-uniform skips of the dead waves and zero slots
-        // still 0.771 / 5.29 ms (profiles/r06/split_ab.txt), so this form stays
-#pragma unroll
-        for (int i = 0; i < G; ++i) {
-            __builtin_amdgcn_sched_barrier(0);   // 3 source limbs per pair, a slot at a time
-            const bool z = zero_in(i);
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int pp = t + NT * r;
-                x[i][r] = Pr{{0, 0, 0, 0}, 0};
-                if (z) continue;
-                const u64 left = (u64)pp * 128 < a.bits1 ? a.bits1 - (u64)pp * 128 : 0;   // bits of the coefficient here
+        // pair pp of a split coefficient from the three source limbs q .. q + 2 holding its bits
+        auto split_pair = [](u64 x0, u64 x1, u64 x2, int sh, u64 left) -> Pr {
+            u64 f0 = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
+            u64 f1 = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
+            f0 = left < 64 ? f0 & ((((u64)1) << left) - 1) : f0;
+            f1 = left <= 64 ? 0 : left < 128 ? f1 & ((((u64)1) << (left - 64)) - 1) : f1;
+            return pr_make(rp_v4u{(u32)f0, (u32)(f0 >> 32), (u32)f1, (u32)(f1 >> 32)}, 0);
+        };
+        // staged form (whole operands): every live slot's source span -- bits1 < N/2 bits, so at most
+        // l/2 + 2 limbs from the even limb below its first -- read with coalesced 16-B loads by
+        // consecutive threads, all slots' loads in flight at once, parked in the exchange slots; each
+        // thread then reads its three limbs per pair back from LDS
+        constexpr int SWP = l / 4 + 2, SW = 2 * SWP, KR = (G * SWP + NT - 1) / NT;
+        constexpr bool STAGE = RP_SPLIT_LDS && (size_t)G * SW * 8 <= (size_t)NX * RX<PP>::SB;
+        if (STAGE && !a.src_chunk) {
+            u64 *S = (u64 *)smem;
+            const long nsv = a.nsrc[op];
+            auto slot_q0 = [&](int i) -> long {   // the even source limb staged slot i starts at
                 const long j = (long)(a.pos_off + g.pos0 + i * g.pstep) * a.jNC + a.sub_off + sub;
-                const u64 off = (u64)j * a.bits1 + (u64)pp * 128;
-                const long q = (long)(off >> 6);
-                const int sh = (int)(off & 63);
-                const long ns = left ? a.nsrc[op] : 0;
-                const SrcSlice sv{a.src_chunk, a.jNC, a.sub_off};
-                const u64 x0 = src_limb(src, ns, sv, j, a.bits1, q), x1 = src_limb(src, ns, sv, j, a.bits1, q + 1),
-                          x2 = src_limb(src, ns, sv, j, a.bits1, q + 2);
-                u64 f0 = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
-                u64 f1 = sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1;
-                f0 = left < 64 ? f0 & ((((u64)1) << left) - 1) : f0;
-                f1 = left <= 64 ? 0 : left < 128 ? f1 & ((((u64)1) << (left - 64)) - 1) : f1;
-                x[i][r] = pr_make(rp_v4u{(u32)f0, (u32)(f0 >> 32), (u32)f1, (u32)(f1 >> 32)}, 0);
+                return (long)(((u64)j * a.bits1) >> 6) & ~1L;
+            };
+            rp_v4u v[KR];
+#pragma unroll
+            for (int k = 0; k < KR; ++k) {
+                const int idx = t + NT * k, i = idx / SWP, u = idx - i * SWP;
+                v[k] = rp_v4u{0, 0, 0, 0};
+                if (i < G && !zero_in(i)) {
+                    const long q = slot_q0(i) + 2 * u;
+                    if (q + 1 < nsv) {
+                        v[k] = *(const rp_v4u *)(src + q);
+                    } else if (q < nsv) {
+                        const u64 w = src[q];
+                        v[k] = rp_v4u{(u32)w, (u32)(w >> 32), 0, 0};
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < KR; ++k) {
+                const int idx = t + NT * k, i = idx / SWP, u = idx - i * SWP;
+                if (i < G && !zero_in(i)) *(rp_v4u *)(S + (long)i * SW + 2 * u) = v[k];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < G; ++i) {
+                const bool z = zero_in(i);
+                const long j = (long)(a.pos_off + g.pos0 + i * g.pstep) * a.jNC + a.sub_off + sub;
+                const long qa = (long)(((u64)j * a.bits1) >> 6) & ~1L;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int pp = t + NT * r;
+                    x[i][r] = Pr{{0, 0, 0, 0}, 0};
+                    const u64 left = (u64)pp * 128 < a.bits1 ? a.bits1 - (u64)pp * 128 : 0;
+                    if (z || !left) continue;
+                    const u64 off = (u64)j * a.bits1 + (u64)pp * 128;
+                    const u64 *sp = S + (long)i * SW + ((long)(off >> 6) - qa);
+                    x[i][r] = split_pair(sp[0], sp[1], sp[2], (int)(off & 63), left);
+                }
+            }
+            __syncthreads();   // the staging area is the exchange slots level 1 publishes into
+        } else {
+            // one slot at a time, guarded loads (a zero slot, and the lanes past the coefficient's
+            // bits1 bits -- the upper half of every split coefficient -- issue none).  Round 5 put four
+            // slots' loads in flight from clamped addresses: C3's pass 0.735 -> 0.885 ms, C4's 5.17 ->
+            // 6.05 (every dead lane loaded); with wave-uniform skips of the dead waves and zero slots
+            // still 0.771 / 5.29 ms (profiles/r06/split_ab.txt)
+#pragma unroll
+            for (int i = 0; i < G; ++i) {
+                __builtin_amdgcn_sched_barrier(0);   // 3 source limbs per pair, a slot at a time
+                const bool z = zero_in(i);
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int pp = t + NT * r;
+                    x[i][r] = Pr{{0, 0, 0, 0}, 0};
+                    if (z) continue;
+                    const u64 left = (u64)pp * 128 < a.bits1 ? a.bits1 - (u64)pp * 128 : 0;   // bits of the coefficient here
+                    const long j = (long)(a.pos_off + g.pos0 + i * g.pstep) * a.jNC + a.sub_off + sub;
+                    const u64 off = (u64)j * a.bits1 + (u64)pp * 128;
+                    const long q = (long)(off >> 6);
+                    const long ns = left ? a.nsrc[op] : 0;
+                    const SrcSlice sv{a.src_chunk, a.jNC, a.sub_off};
+#if RP_SPLIT_PROBE   // timing probe (A/B builds only, wrong products): the split pass without its source loads
+                    const u64 x0 = left ? (u64)q * 0x9e3779b97f4a7c15ull : 0, x1 = x0 ^ (u64)j, x2 = x1 + 1;
+#else
+                    const u64 x0 = src_limb(src, ns, sv, j, a.bits1, q), x1 = src_limb(src, ns, sv, j, a.bits1, q + 1),
+                              x2 = src_limb(src, ns, sv, j, a.bits1, q + 2);
+#endif
+                    x[i][r] = split_pair(x0, x1, x2, (int)(off & 63), left);
+                }
             }
         }
     }
@@ -827,17 +896,31 @@ __global__ __launch_bounds__(rp_nt(1024 * PP, LOGG, DIR), 4) void k_rpass(PassAr
             continue;
         }
         // partner x_k read rotated by E: (x_i, x_k) <- (x_i + 2^E x_k, x_i - 2^E x_k)
+        // Split pass: the input slots at or past zero_from are zero (zero_in is monotone in the
+        // slot), so before DIF level li >= 1 slot s is zero iff input slot s mod 2^(LOGG - li)
+        // was.  A zero partner is neither published nor read: (x_i, x_k) <- (x_i, x_i), bit for
+        // bit what the butterfly gives (workgroup-uniform; C3's pass-0 groups hold 4-5 live
+        // slots of 16, so level 1 exchanges 0-2 of its 8 pairs)
+        auto pz = [&](int k) -> bool { return RP_SPLIT_ZSKIP && SPLIT && zero_in(k & ((1 << (LOGG - li)) - 1)); };
         const int tl = rp_launder(t);
+        bool xch = false;
 #pragma unroll
         for (int pi = 0; pi < G / 2; ++pi) {
             const int i = ((pi >> JB) << (JB + 1)) | (pi & ((1 << JB) - 1));
+            if (pz(i | (1 << JB))) continue;
             rp_pub<PP, NT>(X, pi, x[i | (1 << JB)], tl);
+            xch = true;
         }
-        __syncthreads();
+        if (xch) __syncthreads();
 #pragma unroll
         for (int pi = 0; pi < G / 2; ++pi) {
             const int i = ((pi >> JB) << (JB + 1)) | (pi & ((1 << JB) - 1));
             const int k = i | (1 << JB);
+            if (pz(k)) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) x[k][r] = x[i][r];
+                continue;
+            }
             const u32 E = rp_uniform(EXPT[2 * G + (G / 2) * li + pi]);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -847,7 +930,7 @@ __global__ __launch_bounds__(rp_nt(1024 * PP, LOGG, DIR), 4) void k_rpass(PassAr
                 pr_bfly(x[i][r], x[k][r], x[i][r], y, ng);
             }
         }
-        __syncthreads();
+        if (xch) __syncthreads();
         if (li < 3) RP_STAMP(2 + li);
     }
     // the pending exponents of the last level (whole pairs): one aligned rotation round -- none
