@@ -255,6 +255,11 @@ __global__ __launch_bounds__(256) void k_cmeta(FoldArgs a)
 // one limb (the limb below a block, for its overflow): every load of it -- KM coefficients'
 // window words and mask words, the A / B terms' meta words -- issued before any is used (a
 // fixed-trip loop of guarded loads, as comb_limb: thread 0 runs this while the block waits)
+// timing probes (A/B builds only, wrong products): bit 0 no limb below the block (fold_limb), bit 1 no
+// carries from the masks, bit 2 no A / B terms
+#ifndef FOLD_PROBE
+#define FOLD_PROBE 0
+#endif
 template <int KM>
 __device__ void fold_limb(const FoldArgs &a, long m, u64 *plo, int *phi)
 {
@@ -404,7 +409,7 @@ __device__ __forceinline__ void fold_thread8(const FoldArgs &a, long mW, long mA
     }
     // the carries (at bit (64 - r) mod 64 of limb i) and the A_k 2^N, B_k terms: coefficient k's
     // B at bit k bits1 and A at k bits1 + N lie in this wave's bits only for k in [klo, khi]
-    const u64 PL = (u64)mA * 64;
+    const u64 PL = (u64)mA * 64, PW = (u64)mW * 64;
 #pragma unroll
     for (int j = 0; j < KM; ++j) {
         const long k = klo + j;
@@ -428,7 +433,7 @@ __device__ __forceinline__ void fold_thread8(const FoldArgs &a, long mW, long mA
             const u32 vm = (lb >= 8 || ub <= 0) ? 0u : ((ub >= 8 ? 0xffu : (1u << ub) - 1u) & ~((1u << lb) - 1u));
             cb = ((u32)pbits & vm) | (((u32)nbits & vm) << 8);
         }
-        if (__ballot(cb != 0)) {   // branch-free per limb: d 2^shc with d in {-1, 0, 1} (shc wave-uniform)
+        if ((FOLD_PROBE & 2) == 0 && __ballot(cb != 0)) {   // branch-free per limb: d 2^shc with d in {-1, 0, 1} (shc wave-uniform)
             const int shc = (64 - r) & 63;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
@@ -439,25 +444,35 @@ __device__ __forceinline__ void fold_thread8(const FoldArgs &a, long mW, long mA
                 hi[i] += (u32)((c ? 1 : 0) - (dd < 0 ? 1 : 0));
             }
         }
-        // A_k 2^N and B_k: each lands in one lane of the waves it reaches -- the 128-bit value
-        // formed once, added to the limb it names by selects.  Bits k bits1 and k bits1 + N are N
-        // (> a wave's 512 limbs) apart, so a wave holds at most one of the two: one select pass
-        const int vB = meta_B(mt[j]), vA = meta_A(mt[j]);
+        // A_k 2^N and B_k: bits k bits1 + N and k bits1, N (> a wave's 512 limbs) apart, so a wave
+        // holds at most one of the two, in one lane, at a wave-uniform position: the term is formed
+        // on the scalar side and added to the limb it names by a uniform switch (the per-lane select
+        // over all 8 limbs cost 24 us of C3's combine, profiles/r06/probes.txt)
+        const int mu = __builtin_amdgcn_readfirstlane(mt[j]);
+        const int vB = meta_B(mu), vA = meta_A(mu);
         const u64 ka = kb + a.N;
-        const bool inB = vB && kb >= PL && kb < PL + 512, inA = vA && ka >= PL && ka < PL + 512;
-        if (__ballot(inB || inA)) {
-            const bool in = inB || inA;
-            const i64 x = inB ? vB : inA ? vA : 0;
-            const int bb = in ? (int)((inB ? kb : ka) - PL) : 0, li = bb >> 6, b = bb & 63;
-            const u64 xl = (u64)x << b;
-            const u32 xh = (u32)(b ? (x >> (64 - b)) : (x < 0 ? -1 : 0));
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const bool m = i == li;
+        const bool inB = vB && kb >= PW && kb < PW + 32768, inA = vA && ka >= PW && ka < PW + 32768;
+        if (inB || inA) {
+            const i64 x = inB ? vB : vA;
+            const u64 bp = (inB ? kb : ka) - PW;   // bit within the wave's 512 limbs
+            const int Ls = (int)(bp >> 9), li = __builtin_amdgcn_readfirstlane((int)((bp >> 6) & 7)), b = (int)(bp & 63);
+            const u64 xl = L == Ls ? (u64)x << b : 0;
+            const u32 xh = L == Ls ? (u32)(b ? (x >> (64 - b)) : (x < 0 ? -1 : 0)) : 0u;
+            auto add_at = [&](int i) {
                 u64 t;
-                const bool c = add_ovf(lo[i], m ? xl : 0, &t);
+                const bool c = add_ovf(lo[i], xl, &t);
                 lo[i] = t;
-                hi[i] += (m ? xh : 0u) + (c ? 1u : 0u);
+                hi[i] += xh + (c ? 1u : 0u);
+            };
+            switch (li) {
+            case 0: add_at(0); break;
+            case 1: add_at(1); break;
+            case 2: add_at(2); break;
+            case 3: add_at(3); break;
+            case 4: add_at(4); break;
+            case 5: add_at(5); break;
+            case 6: add_at(6); break;
+            default: add_at(7); break;
             }
         }
     }
@@ -496,7 +511,7 @@ __global__ __launch_bounds__(NT, KM <= 3 ? 2048 / NT : 1) void k_combine_red(Fol
     if (t == 0) {
         u64 l0 = 0;
         int h0 = 0;
-        if (base > 0 && base < total) fold_limb<KM>(a, base - 1, &l0, &h0);
+        if ((FOLD_PROBE & 1) == 0 && base > 0 && base < total) fold_limb<KM>(a, base - 1, &l0, &h0);
         H[0] = h0;
     }
     __syncthreads();
