@@ -458,14 +458,32 @@ __device__ __forceinline__ void pw_combine_fixed(u64 (&L)[M], int &T, int &S, in
     }
 }
 
+#ifndef PW_UNW_FUSE
+#define PW_UNW_FUSE 1   // 0 (A/B builds): the un-weighting as its own publish + rotated read after the inverse
+#endif
 #ifndef PW_PROBE_NOH1
 #define PW_PROBE_NOH1 0   // 1: timing probe, the h = 1 levels without their LDS round (A/B builds only)
 #endif
 // one level jj of the transform.  FIXJ >= 0 (forward transforms, level jj = FIXJ): E mod N' is
 // wave-uniform and one of 2^FIXJ compile-time values (level 0: exactly N'/2) -- pw_transform
-template <int M, int LK, int DIR, int FIXJ>
+// UNW (the inverse's last level, h = K/2): the un-weighting theta^-t 2^-lk folded in -- with F the
+// exponent it applies after the level (pw_unweight_exp), r = alpha 2^F own + 2^(E + F) x_q: own is
+// read back rotated from the words it has just published for its partner, so the separate publish +
+// rotated read of the un-weighting is gone (pw_slot_product)
+template <int M, int LK>
+__device__ __forceinline__ unsigned pw_unweight_exp(unsigned Pz, unsigned W2, int t)
+{
+    constexpr unsigned NP = 64 * M, N2 = 2 * NP;
+    // theta^-t 2^-lk: 2^-(t W2 / 2 + lk), for a half-integer t W2 / 2 (sqrt 2)^-1 = sqrt 2 / 2:
+    // 2^(-floor(t W2 / 2) - 1 - lk + N'/4) (2^(N'/2) - 1) -- the (2^(N'/2) - 1) factor by the caller
+    const bool halff = (W2 & 1) && (t & 1);
+    const unsigned un = (((unsigned)t * W2) >> 1) + LK + (halff ? 1 : 0);   // < N' + lk + 1
+    return pw_mod(Pz + N2 - un + (halff ? NP / 4 : 0), N2);
+}
+
+template <int M, int LK, int DIR, int FIXJ, bool UNW = false>
 __device__ __forceinline__ void pw_level(u64 (&L)[M], int &T, int &S, unsigned &P, u32 *Xw, int *TT, unsigned *PP,
-                                         unsigned W2, int t, int jj)
+                                         unsigned W2, int t, int jj, bool unw = false)
 {
     constexpr int K = 1 << LK, lk = LK;
     constexpr unsigned N2 = 128 * M;
@@ -517,6 +535,7 @@ __device__ __forceinline__ void pw_level(u64 (&L)[M], int &T, int &S, unsigned &
         Pq = PP[q];
         packed = TT[q];
     }
+    const int own_packed = 2 * T + S;   // (UNW) as published: T normalised by pw_publish / pw_norm
     unsigned E;
     if (DIR == 0) {
         // top: X_t + X_q = 2^P (x_t + 2^(Pq-P) x_q); bottom: (X_q - X_t) w^tw = 2^(P+tw) (2^(Pq-P) x_q - x_t)
@@ -536,8 +555,19 @@ __device__ __forceinline__ void pw_level(u64 (&L)[M], int &T, int &S, unsigned &
         // top: Z_t + Z_q w^-tw = 2^P (z_t + 2^(Pq-tw-P) z_q)
         // bottom: Z_q - Z_t w^-tw = 2^(P-tw) (2^(Pq-P+tw) z_q - z_t)
         E = top ? pw_mod(Pq + 2 * N2 - tw - P, N2) : pw_mod(Pq + N2 - P + tw, N2);
-        pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, top ? 1 : -1, Xw, packed, q, E);
-        if (!top) P = pw_mod(P + N2 - tw, N2);
+        if (UNW && unw) {
+            if (!top) P = pw_mod(P + N2 - tw, N2);
+            const unsigned F = pw_unweight_exp<M, LK>(P, W2, pw_tight(K) ? pw_launder(t) : t);
+            constexpr unsigned NP = 64 * M;
+            const unsigned Eq = pw_mod(E + F, N2);
+            pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, 0, Xw, own_packed, t, top ? F : pw_mod(F + NP, N2));
+            __builtin_amdgcn_sched_barrier(0);   // the two rotated reads one after the other
+            pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, 1, Xw, packed, q, Eq);
+            P = 0;
+        } else {
+            pw_combine<M, LK, pw_pd<M, LK>()>(L, T, S, top ? 1 : -1, Xw, packed, q, E);
+            if (!top) P = pw_mod(P + N2 - tw, N2);
+        }
     }
     if (cross) __syncthreads(); else pw_wave_sync();
 }
@@ -669,7 +699,7 @@ __device__ __forceinline__ void pw_transform(u64 (&L)[M], int &T, int &S, unsign
     if constexpr (DIR == 0 && PW_R4_FWD && !pw_tight(1 << LK)) {
         for (; jj + 1 < LK; jj += 2) pw_level4_dif<M, LK>(L, T, S, P, Xw, TT, PP, W2, t, jj);
     }
-    for (; jj < LK; ++jj) pw_level<M, LK, DIR, -1>(L, T, S, P, Xw, TT, PP, W2, t, jj);
+    for (; jj < LK; ++jj) pw_level<M, LK, DIR, -1, DIR == 1 && PW_UNW_FUSE>(L, T, S, P, Xw, TT, PP, W2, t, jj, jj == LK - 1);
 }
 
 // Piece t of a coefficient in the reduced HBM form (coeff.hpp: limbs + carry masks +
@@ -936,7 +966,13 @@ __device__ __forceinline__ void pw_slot_product(u64 (&La)[M], int Ta, u64 (&Lb)[
     // ---- inverse, then 2^-lk (division by K) and theta^-t --------------------------
     pw_transform<M, LK, 1>(Z, Tz, Sz, Pz, Xw, TT, PP, W2, t);
     PW_STAMP(5);
-    {
+    if constexpr (PW_UNW_FUSE && !(PW_R4_INV && !pw_tight(K) && LK % 2 == 0)) {
+        // the rotation by theta^-t 2^-lk rode in the last level (pw_level UNW); the (2^(N'/2) - 1)
+        // of a half-integer weight commutes with it (that level ended with a barrier: the u64 rows
+        // below may cross columns)
+        const int tf = pw_tight(K) ? pw_launder(t) : t;
+        if ((W2 & 1) && (tf & 1)) pw_sqrt2<M>(Z, Tz);
+    } else {
         // theta^-t 2^-lk: 2^-(t W2 / 2 + lk), for a half-integer t W2 / 2 (sqrt 2)^-1 = sqrt 2 / 2:
         // 2^(-floor(t W2 / 2) - 1 - lk + N'/4) (2^(N'/2) - 1)
         const int tf = pw_tight(K) ? pw_launder(t) : t;   // (at l = 2048 the laundered form measured 1 % slower)
