@@ -99,12 +99,13 @@ __device__ __forceinline__ int meta_B(int m) { return m >> 16; }
 // lies in [0, p) for any small Xhi and m = Xhi (and with a zero top limb too when Xhi <= 0, with
 // an all-ones one when Xhi >= -1).  Otherwise (adversarial inputs: runs of 0 or all-ones limbs)
 // the whole wave resolves that coefficient (cmeta_full).
+template <int NL>   // NL = l / 64 limbs per lane held in registers (one round trip); 0: runtime l, batches of 8
 __device__ int cmeta_full(const FoldArgs &a, long k, int lane)
 {
     // lane L resolves limbs [L nl, (L + 1) nl): its limbs' composite transfer function (one
     // sequential sweep), a wave scan for the carries into the lanes, a second sweep for the
     // resolved limbs
-    const int l = a.l, nl = l >> 6;
+    const int l = a.l, nl = NL ? NL : l >> 6;
     const u64 *d = a.dig + k * (long)l;
     const u64 *cb = a.cb + k * (long)a.cbw;
     const int s = fold_s(a, k);
@@ -138,14 +139,30 @@ __device__ int cmeta_full(const FoldArgs &a, long k, int lane)
         return (c == 1 && x == MPF_MAXL) ? 1 : (c == -1 && x == 0) ? -1 : 0;
     };
     u32 F = CF_ID;
-    for (int i = i0; i < i0 + nl; i += 8) {
-        u64 x[8];
-        batch(i, x);
+    u64 xa[NL ? NL : 1];
+    if constexpr (NL > 0) {   // every limb of the lane requested at once, kept for the second sweep
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
+        for (int q = 0; q < NL; q += 2) {
+            const cb_v2u v = *(const cb_v2u *)(d + i0 + q);
+            xa[q] = v.x;
+            xa[q + 1] = v.y;
+        }
+#pragma unroll
+        for (int q = 0; q < NL; ++q) {
             u64 u;
-            const int g = limb(i + q, x[q], u);
+            const int g = limb(i0 + q, xa[q], u);
             F = cf_then(F, cf_make(g, u));
+        }
+    } else {
+        for (int i = i0; i < i0 + nl; i += 8) {
+            u64 x[8];
+            batch(i, x);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                u64 u;
+                const int g = limb(i + q, x[q], u);
+                F = cf_then(F, cf_make(g, u));
+            }
         }
     }
     const u32 I = cf_wave_scan(F, lane);
@@ -154,23 +171,29 @@ __device__ int cmeta_full(const FoldArgs &a, long k, int lane)
     int c = cf_apply(E, 0);   // carry into limb i0 (none into limb 0)
     bool allz = true, allo = true;
     u64 Rfirst = 0, R = 0, prev = 0;
-    for (int i = i0; i < i0 + nl; i += 8) {
-        u64 x[8];
-        batch(i, x);
+    auto resolve = [&](int i, u64 xv) {   // limb i (>= i0) with the carry c from below
+        u64 u;
+        const int g = limb(i, xv, u);
+        R = u + (u64)(i64)c;
+        c = cf_apply(cf_make(g, u), c);
+        if (i == i0) {
+            Rfirst = R;
+        } else {
+            const u64 X = s ? (R << 1) | (prev >> 63) : R;   // Xlo's limb i (>= 1)
+            allz = allz && X == 0;
+            allo = allo && X == MPF_MAXL;
+        }
+        prev = R;
+    };
+    if constexpr (NL > 0) {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            u64 u;
-            const int g = limb(i + q, x[q], u);
-            R = u + (u64)(i64)c;
-            c = cf_apply(cf_make(g, u), c);
-            if (i + q == i0) {
-                Rfirst = R;
-            } else {
-                const u64 X = s ? (R << 1) | (prev >> 63) : R;   // Xlo's limb i + q (>= 1)
-                allz = allz && X == 0;
-                allo = allo && X == MPF_MAXL;
-            }
-            prev = R;
+        for (int q = 0; q < NL; ++q) resolve(i0 + q, xa[q]);
+    } else {
+        for (int i = i0; i < i0 + nl; i += 8) {
+            u64 x[8];
+            batch(i, x);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) resolve(i + q, x[q]);
         }
     }
     u64 pl = __shfl_up(R, 1);   // the limb below i0
@@ -197,6 +220,7 @@ __device__ __forceinline__ void cmeta_store(const FoldArgs &a, long k, int A, in
     a.meta[k] = (A & 0xffff) | (int)((unsigned)B << 16);
 }
 
+template <int NL>   // l / 64 for l = 1024 / 2048 / 4096 (the slow path's limbs per lane in registers), 0 any l
 __global__ __launch_bounds__(256) void k_cmeta(FoldArgs a)
 {
     const int lane = threadIdx.x & 63;
@@ -236,7 +260,7 @@ __global__ __launch_bounds__(256) void k_cmeta(FoldArgs a)
         const int ln = __builtin_ctzll(rest);
         rest &= rest - 1;
         const long kk = kw + ln;
-        const int A = cmeta_full(a, kk, lane);
+        const int A = cmeta_full<NL>(a, kk, lane);
         if (lane == 0) {
             const int s = fold_s(a, kk);
             const u64 *cb = a.cb + kk * (long)a.cbw;

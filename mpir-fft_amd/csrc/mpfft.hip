@@ -1306,7 +1306,8 @@ struct Exec {
         a.bps = (P.total + 8 * NT - 1) / (8 * NT);
         u32 *st = comb_flags(ws);
         if (zflags != st) HIPCHK(hipMemsetAsync(st, 0, (size_t)(a.bps + 1) * 4, s));
-        hipLaunchKernelGGL(k_cmeta, dim3((unsigned)((P.len + 255) / 256)), dim3(256), 0, s, a);   // a lane per coefficient
+        auto cm = P.l == 1024 ? k_cmeta<16> : P.l == 2048 ? k_cmeta<32> : P.l == 4096 ? k_cmeta<64> : k_cmeta<0>;
+        hipLaunchKernelGGL(cm, dim3((unsigned)((P.len + 255) / 256)), dim3(256), 0, s, a);   // a lane per coefficient
         HIPCHK(hipGetLastError());
         void (*f)(FoldArgs, u64 *, u32 *) = P.fold == 3 ? k_combine_red<3, NT> : k_combine_red<4, NT>;
         hipLaunchKernelGGL(f, dim3((unsigned)a.bps), dim3(NT), 0, s, a, r, st);
