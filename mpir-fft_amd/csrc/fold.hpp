@@ -281,6 +281,9 @@ __global__ __launch_bounds__(256) void k_cmeta(FoldArgs a)
 // fixed-trip loop of guarded loads, as comb_limb: thread 0 runs this while the block waits)
 // timing probes (A/B builds only, wrong products): bit 0 no limb below the block (fold_limb), bit 1 no
 // carries from the masks, bit 2 no A / B terms
+#ifndef FOLD_PERSIST
+#define FOLD_PERSIST 1   // 0 (A/B builds): one workgroup per ticket, a grid of bps blocks
+#endif
 #ifndef FOLD_PROBE
 #define FOLD_PROBE 0
 #endif
@@ -518,103 +521,119 @@ __global__ __launch_bounds__(NT, KM <= 3 ? 2048 / NT : 1) void k_combine_red(Fol
     __shared__ cb_v2u MS[NW][KM][9];
     __shared__ u32 sh_b;
     __shared__ int sh_cin;
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    if (t == 0) sh_b = __hip_atomic_fetch_add(&st[gridDim.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const long nb = a.bps;   // st[nb]: the ticket counter
+    if (threadIdx.x == 0) sh_b = __hip_atomic_fetch_add(&st[nb], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    const long b = sh_b;   // ticket: every block below it has started
-    const long total = a.total;
-    const long base = b * CB;
-    u64 lo[8];
-    u32 hu[8];
-    const int t0 = __builtin_amdgcn_readfirstlane(t & ~63);
-    fold_thread8<KM>(a, base + 8L * t0, base + 8L * t, total, lo, hu, XS[wave], MS[wave]);
-    int hi[8];
+    // persistent (FOLD_PERSIST: a grid of about the resident block count): a workgroup takes tickets
+    // until they run out, the next one requested at the start of this one's work so its round trip
+    // hides under the loads; each ticket's work is the one-block body below
+    for (;;) {
+        // the thread index as an opaque value per ticket: what derives from it is recomputed, not
+        // kept live across the loop (hoisted, it spilled 44 B per lane)
+        int t = threadIdx.x;
+        asm volatile("" : "+v"(t));
+        const int lane = t & 63, wave = t >> 6;
+        const long b = sh_b;   // ticket: every block below it has started
+        if (b >= nb) break;   // workgroup-uniform
+        u32 nxt = 0;
+        if (t == 0) nxt = __hip_atomic_fetch_add(&st[nb], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const long total = a.total;
+        const long base = b * CB;
+        u64 lo[8];
+        u32 hu[8];
+        const int t0 = __builtin_amdgcn_readfirstlane(t & ~63);
+        fold_thread8<KM>(a, base + 8L * t0, base + 8L * t, total, lo, hu, XS[wave], MS[wave]);
+        int hi[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) hi[k] = (int)hu[k];
-    H[t + 1] = hi[7];
-    if (t == 0) {
-        u64 l0 = 0;
-        int h0 = 0;
-        if ((FOLD_PROBE & 1) == 0 && base > 0 && base < total) fold_limb<KM>(a, base - 1, &l0, &h0);
-        H[0] = h0;
-    }
-    __syncthreads();
-    u64 u[8];
-    u32 gk = 0;   // limb k's local carry + 1 at bits 2k (3: past the end, transparent)
-#pragma unroll
-    for (int k = 0; k < V; ++k) {
-        const bool real = base + 8L * t + k < total;
-        const int hin = k ? hi[k - 1] : H[t];
-        const u64 v = lo[k] + (u64)(i64)hin;
-        const int g = hin >= 0 ? (v < lo[k] ? 1 : 0) : (v > lo[k] ? -1 : 0);
-        u[k] = v;
-        gk |= (real ? (u32)(g + 1) : 3u) << (2 * k);
-    }
-    auto fk = [&](int k) -> u32 {
-        const u32 gq = (gk >> (2 * k)) & 3u;
-        return gq == 3u ? CF_ID : cf_make((int)gq - 1, u[k]);
-    };
-    // the thread's composite, last limb first: a limb that neither is 0 nor all ones maps every
-    // carry-in to its own carry, so the composite almost always stops at limb 7
-    u32 F = fk(7);
-#pragma unroll
-    for (int k = 6; k >= 0; --k)
-        if (!cf_const(F)) F = cf_then(fk(k), F);
-    u32 I, Ex;
-    if (__ballot(!cf_const(F)) == 0) {   // every lane constant: lane L's carry-in is lane L - 1's carry-out
-        I = F;
-        Ex = (u32)__shfl_up((int)F, 1);
-    } else {
-        I = cf_wave_scan(F, lane);
-        Ex = (u32)__shfl_up((int)I, 1);
-    }
-    if (lane == 0) Ex = CF_ID;
-    if (lane == 63) WF[wave] = I;
-    __syncthreads();
-    // the composites of the waves below (Wp) and of the block (Fb); a constant wave function
-    // overrides everything before it, the common case
-    u32 Wp = CF_ID, Fb = CF_ID;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-        const u32 f = WF[w];
-        const u32 nb = cf_const(f) ? f : cf_then(Fb, f);
-        if (w < wave) Wp = nb;
-        Fb = nb;
-    }
-    if (t == 0) {
-        int cin = 0;
-        if (b == 0) {
-            __hip_atomic_store(&st[0], 9u + (u32)cf_apply(Fb, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            const bool cst = cf_const(Fb);
-            __hip_atomic_store(&st[b], cst ? 9u + (u32)cf_apply(Fb, 0) : 16u + Fb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            u32 acc = CF_ID;
-            for (long q = b - 1;; --q) {
-                u32 f;
-                while ((f = __hip_atomic_load(&st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u)
-                    __builtin_amdgcn_s_sleep(1);
-                if (f < 16u) {
-                    cin = cf_apply(acc, (int)f - 9);
-                    break;
-                }
-                acc = cf_then(f - 16u, acc);
-            }
-            if (!cst) __hip_atomic_store(&st[b], 9u + (u32)cf_apply(Fb, cin), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int k = 0; k < 8; ++k) hi[k] = (int)hu[k];
+        H[t + 1] = hi[7];
+        if (t == 0) {
+            u64 l0 = 0;
+            int h0 = 0;
+            if ((FOLD_PROBE & 1) == 0 && base > 0 && base < total) fold_limb<KM>(a, base - 1, &l0, &h0);
+            H[0] = h0;
         }
-        sh_cin = cin;
-    }
-    __syncthreads();
-    int c = cf_apply(cf_then(Wp, Ex), sh_cin);
+        __syncthreads();
+        u64 u[8];
+        u32 gk = 0;   // limb k's local carry + 1 at bits 2k (3: past the end, transparent)
 #pragma unroll
-    for (int k = 0; k < V; ++k) {
-        Lx[t * V + k] = u[k] + (u64)(i64)c;
-        const int gq = (int)((gk >> (2 * k)) & 3u) - 1;   // 2: past the end (transparent)
-        c = gq == 2 ? c : gq + (c == 1 && u[k] == MPF_MAXL) - (c == -1 && u[k] == 0);
-    }
-    __syncthreads();
+        for (int k = 0; k < V; ++k) {
+            const bool real = base + 8L * t + k < total;
+            const int hin = k ? hi[k - 1] : H[t];
+            const u64 v = lo[k] + (u64)(i64)hin;
+            const int g = hin >= 0 ? (v < lo[k] ? 1 : 0) : (v > lo[k] ? -1 : 0);
+            u[k] = v;
+            gk |= (real ? (u32)(g + 1) : 3u) << (2 * k);
+        }
+        auto fk = [&](int k) -> u32 {
+            const u32 gq = (gk >> (2 * k)) & 3u;
+            return gq == 3u ? CF_ID : cf_make((int)gq - 1, u[k]);
+        };
+        // the thread's composite, last limb first: a limb that neither is 0 nor all ones maps every
+        // carry-in to its own carry, so the composite almost always stops at limb 7
+        u32 F = fk(7);
 #pragma unroll
-    for (int k = 0; k < V; ++k) {
-        const long m = base + k * NT + t;
-        if (m < total) r[m] = Lx[k * NT + t];
+        for (int k = 6; k >= 0; --k)
+            if (!cf_const(F)) F = cf_then(fk(k), F);
+        u32 I, Ex;
+        if (__ballot(!cf_const(F)) == 0) {   // every lane constant: lane L's carry-in is lane L - 1's carry-out
+            I = F;
+            Ex = (u32)__shfl_up((int)F, 1);
+        } else {
+            I = cf_wave_scan(F, lane);
+            Ex = (u32)__shfl_up((int)I, 1);
+        }
+        if (lane == 0) Ex = CF_ID;
+        if (lane == 63) WF[wave] = I;
+        __syncthreads();
+        // the composites of the waves below (Wp) and of the block (Fb); a constant wave function
+        // overrides everything before it, the common case
+        u32 Wp = CF_ID, Fb = CF_ID;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            const u32 f = WF[w];
+            const u32 nb = cf_const(f) ? f : cf_then(Fb, f);
+            if (w < wave) Wp = nb;
+            Fb = nb;
+        }
+        if (t == 0) {
+            int cin = 0;
+            if (b == 0) {
+                __hip_atomic_store(&st[0], 9u + (u32)cf_apply(Fb, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                const bool cst = cf_const(Fb);
+                __hip_atomic_store(&st[b], cst ? 9u + (u32)cf_apply(Fb, 0) : 16u + Fb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                u32 acc = CF_ID;
+                for (long q = b - 1;; --q) {
+                    u32 f;
+                    while ((f = __hip_atomic_load(&st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u)
+                        __builtin_amdgcn_s_sleep(1);
+                    if (f < 16u) {
+                        cin = cf_apply(acc, (int)f - 9);
+                        break;
+                    }
+                    acc = cf_then(f - 16u, acc);
+                }
+                if (!cst) __hip_atomic_store(&st[b], 9u + (u32)cf_apply(Fb, cin), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            sh_cin = cin;
+        }
+        __syncthreads();
+        int c = cf_apply(cf_then(Wp, Ex), sh_cin);
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            Lx[t * V + k] = u[k] + (u64)(i64)c;
+            const int gq = (int)((gk >> (2 * k)) & 3u) - 1;   // 2: past the end (transparent)
+            c = gq == 2 ? c : gq + (c == 1 && u[k] == MPF_MAXL) - (c == -1 && u[k] == 0);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            const long m = base + k * NT + t;
+            if (m < total) r[m] = Lx[k * NT + t];
+        }
+        __syncthreads();   // every read of this ticket's LDS done
+        if (t == 0) sh_b = nxt;
+        __syncthreads();
     }
 }

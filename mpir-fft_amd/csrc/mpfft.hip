@@ -1310,7 +1310,15 @@ struct Exec {
         hipLaunchKernelGGL(cm, dim3((unsigned)((P.len + 255) / 256)), dim3(256), 0, s, a);   // a lane per coefficient
         HIPCHK(hipGetLastError());
         void (*f)(FoldArgs, u64 *, u32 *) = P.fold == 3 ? k_combine_red<3, NT> : k_combine_red<4, NT>;
-        hipLaunchKernelGGL(f, dim3((unsigned)a.bps), dim3(NT), 0, s, a, r, st);
+        // persistent grid: the resident block count (workgroups take tickets until none are left)
+        long grid = a.bps;
+        if (FOLD_PERSIST) {
+            int per = 0, ncu = 0, dev = 0;
+            if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess
+                && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)f, NT, 0) == hipSuccess && per > 0 && ncu > 0)
+                grid = std::min<long>(grid, (long)per * ncu);
+        }
+        hipLaunchKernelGGL(f, dim3((unsigned)grid), dim3(NT), 0, s, a, r, st);
         HIPCHK(hipGetLastError());
         return MPFFT_OK;
     }
