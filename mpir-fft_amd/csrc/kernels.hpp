@@ -65,6 +65,8 @@ struct PassArgs {
     // mode bit 2): positions p >= fill_lo also store 2^(p fill_rho) x_p at position p + fill_off
     int fill_lo, fill_off;
     u64 fill_rho;
+    int grp0;            // k_rpass DIF: the first live group of a sub-array (the launch covers only the
+                         // live groups, [grp0, grp0 + ngroups): no empty 1024-thread workgroups)
 };
 
 // Grid-stride clear of PassArgs::zp; called at the top of every pass kernel, before
@@ -184,7 +186,7 @@ __global__ __launch_bounds__(MPF_LB(U)) void k_pass(PassArgs a)
     st.cb = a.cb[op];
     st.top = a.top[op];
     const int sub = (int)(blockIdx.x / a.ngroups);
-    const int grp = (int)(blockIdx.x % a.ngroups);
+    const int grp = (int)(a.grp0 + blockIdx.x % a.ngroups);
     const int lobits = a.lbM - a.lvl0 - LOGG;
     const int lo = grp & ((1 << lobits) - 1);
     const int hi = grp >> lobits;

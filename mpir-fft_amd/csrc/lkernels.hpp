@@ -114,7 +114,7 @@ __global__ __launch_bounds__(32 << LOGG) void k_lpass(PassArgs a)
     st.cb = a.cb[op];
     st.top = a.top[op];
     const int sub = (int)(blockIdx.x / a.ngroups);
-    const int grp = (int)(blockIdx.x % a.ngroups);
+    const int grp = (int)(a.grp0 + blockIdx.x % a.ngroups);
     const int lobits = a.lbM - a.lvl0 - LOGG;
     const int lo = grp & ((1 << lobits) - 1);
     const int hi = grp >> lobits;

@@ -553,6 +553,26 @@ struct Exec {
         return P.bp_lg;
     }
 
+    // the groups a pass launches: all 2^(lbM - logg) per sub-array, except in a forward pass, where
+    // only blocks of 2^(lbM - lvl0) positions meeting [need_lo, need) are live -- the kernels return
+    // at once for the others, but a launched-and-returning 1024-thread workgroup with 147 KB of LDS
+    // still cost C3's second column pass 0.3 ms (931 -> 636 us, profiles/r06/live_groups_ab.txt):
+    // the grid covers [grp0, grp0 + ngroups) only
+    static void live_groups(PassArgs &a, int logg, int dir)
+    {
+        a.ngroups = 1 << (a.lbM - logg);
+        a.grp0 = 0;
+        if (dir != 0) return;
+        const int slg = a.lbM - a.lvl0, lobits = slg - logg;
+        const long nh = 1L << a.lvl0;
+        const long hlo = std::min<long>(nh, a.need_lo > 0 ? (long)a.need_lo >> slg : 0);
+        const long hhi = std::min<long>(nh, ((long)a.need + (1L << slg) - 1) >> slg);
+        if (hhi > hlo) {
+            a.grp0 = (int)(hlo << lobits);
+            a.ngroups = (int)((hhi - hlo) << lobits);
+        }
+    }
+
     int pass(PassArgs a, int logg, int dir, int nops)
     {
         const int rm = rp_mode(a, logg, dir);
@@ -564,7 +584,7 @@ struct Exec {
             a.ablate = abl;
             const size_t lds = rp_lds((int)P.l, logg) + pad;   // pad: diagnostics (one workgroup per CU)
             allow_lds((const void *)f, lds);
-            a.ngroups = 1 << (a.lbM - logg);
+            live_groups(a, logg, dir);
             dim3 grid((unsigned)((long)a.nsub * a.ngroups), (unsigned)nops);
             static const bool stamps = diag_env("MPFFT_RP_STAMPS") != nullptr;
             const unsigned nt = (unsigned)rp_nt((int)P.l, logg, dir);
@@ -580,7 +600,7 @@ struct Exec {
             if (!f) return MPFFT_EUNSUPPORTED;
             const size_t lds = bp_lds_need((int)P.l, 1 << logg);
             allow_lds((const void *)f, lds);
-            a.ngroups = 1 << (a.lbM - logg);
+            live_groups(a, logg, dir);
             dim3 grid((unsigned)((long)a.nsub * a.ngroups), (unsigned)nops);
             const unsigned nthr = (unsigned)(64 * bp_waves((int)P.l, logg));
             static const bool stamps = diag_env("MPFFT_BP_STAMPS") != nullptr;
@@ -594,7 +614,7 @@ struct Exec {
             if (!f) return MPFFT_EUNSUPPORTED;
             const size_t lds = ((size_t)16 * P.l) << logg;
             allow_lds((const void *)f, lds);
-            a.ngroups = 1 << (a.lbM - logg);
+            live_groups(a, logg, dir);
             dim3 grid((unsigned)((long)a.nsub * a.ngroups), (unsigned)nops);
             hipLaunchKernelGGL(f, grid, dim3(32 << logg), lds, s, a);
             HIPCHK(hipGetLastError());
@@ -609,7 +629,7 @@ struct Exec {
             if (!f) return MPFFT_EUNSUPPORTED;
             const size_t lds = wpass_lds(P.wU, 1 << logg, (int)P.l);
             allow_lds((const void *)f, lds);
-            a.ngroups = 1 << (a.lbM - logg);
+            live_groups(a, logg, dir);
             const long waves = (long)a.nsub * a.ngroups;
             dim3 grid((unsigned)((waves + WPB - 1) / WPB), (unsigned)nops);
             hipLaunchKernelGGL(f, grid, dim3(64 * WPB), lds, s, a);
@@ -623,7 +643,7 @@ struct Exec {
         const size_t lds_pass = lds_bytes((int)P.l, rb, G, P.U, nw);
         allow_lds((const void *)f, lds_pass);
         a.nbuf = rb;
-        a.ngroups = 1 << (a.lbM - logg);
+        live_groups(a, logg, dir);
         dim3 grid((unsigned)((long)a.nsub * a.ngroups), (unsigned)nops);
         hipLaunchKernelGGL(f, grid, dim3(P.tpb), lds_pass, s, a);
         HIPCHK(hipGetLastError());

@@ -714,7 +714,7 @@ __global__ __launch_bounds__(rp_nt(1024 * PP, LOGG, DIR), 4) void k_rpass(PassAr
     // group geometry is workgroup-uniform: keep it in SGPRs (readfirstlane), the VGPRs
     // are all needed for the coefficients
     const int sub = __builtin_amdgcn_readfirstlane((int)(blockIdx.x / a.ngroups));
-    const int grp = __builtin_amdgcn_readfirstlane((int)(blockIdx.x % a.ngroups));
+    const int grp = __builtin_amdgcn_readfirstlane((int)(a.grp0 + blockIdx.x % a.ngroups));
     const int lobits = a.lbM - a.lvl0 - LOGG;
     const int lo = grp & ((1 << lobits) - 1);
     const int hi = grp >> lobits;

@@ -90,7 +90,7 @@ __global__ __launch_bounds__(64 * WPB) void k_wpass(PassArgs a)
     st.cb = a.cb[op];
     st.top = a.top[op];
     const int sub = (int)(gw / a.ngroups);
-    const int grp = (int)(gw % a.ngroups);
+    const int grp = (int)(a.grp0 + gw % a.ngroups);
     const int lobits = a.lbM - a.lvl0 - LOGG;
     const int lo = grp & ((1 << lobits) - 1);
     const int hi = grp >> lobits;
