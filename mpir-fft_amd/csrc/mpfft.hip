@@ -304,7 +304,8 @@ static void plan_dbl(const Plan &P, long *lo, long *hi)
 
 // The matrix split of the MFA is internal (no internal ABI): the reference takes
 // NC = 2^floor(depth/2) columns (mul_fft.c:3195).  At l = 2048 with truncation case b
-// (trunc > half the convolution) twice the columns with four-level forward passes is faster:
+// (trunc > half the convolution), and since round 6 in case a at depth 13-15 as well (below),
+// twice the columns with four-level forward passes is faster:
 // C3 (depth 15) 256 x 256 runs its 8 column levels in 4 + 4 where 128 x 512 needs 3 + 3 + 3,
 // 8.64 vs 8.81 ms; in case a the reference split's column transform skips its empty upper
 // half and wins (C2: 6.69 vs 6.99 ms); at l = 4096 (C4) 512 x 512 with three-level passes
@@ -316,9 +317,15 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
     // diagnostics (A/B): MPFFT_SPLIT=ref / alt forces a split
     static const char *force = diag_env("MPFFT_SPLIT");
     if (rc || sqrt2 || !p->rpass || p->l != 2048 || (force && !strcmp(force, "ref"))) return rc;
-    if (!(force && !strcmp(force, "alt")) && 2 * p->Tr <= p->NR) return rc;
+    // case a (2 Tr <= NR) too at depth 13-15 since the live-group launches (C2 6.09 -> 5.95 ms, -2.2 to
+    // -4.8 % over truncation ratios 0.40-0.48 at depth 13-15, +0.3-0.5 % at depth 16:
+    // profiles/r06/split_resweep.txt); smaller depths were not re-measured and keep the rule
+    const bool casea = 2 * p->Tr <= p->NR;
+    if (!(force && !strcmp(force, "alt")) && casea && (depth < 13 || depth > 15)) return rc;
     Plan q;
-    if (make_plan_split(&q, n1, n2, depth, w, sqrt2, (int)depth / 2 + 1, true) == MPFFT_OK && q.rpass) *p = q;
+    if (make_plan_split(&q, n1, n2, depth, w, sqrt2, (int)depth / 2 + 1, true) == MPFFT_OK && q.rpass
+        && (!casea || (force && !strcmp(force, "alt")) || q.trunc <= p->trunc + p->trunc / 64))   // case a: at most 1/64 more truncated length
+        *p = q;
     return MPFFT_OK;
 }
 

@@ -330,16 +330,19 @@ def test_fill_fold_l4096_case_b(mp, oracle, depth, w, nl):
     assert (mp.mul(a, b, depth, w) == oracle.gmp_mul(a, b)).all()
 
 
-@pytest.mark.parametrize("depth,w,nl,alt", [(12, 32, 2200000, True), (13, 16, 4500000, True),
-                                            (14, 8, 9000000, True), (13, 16, 3000000, False),
-                                            (5, 4096, 20000, True), (6, 2048, 40000, True),
-                                            (7, 1024, 80000, True)])
-def test_mfa_split_l2048(mp, oracle, depth, w, nl, alt):
-    """The plan's MFA split at l = 2048 (make_plan): truncation case b takes twice the
-    reference's columns (mul_fft.c:3195) with four-level forward k_rpass passes (7 row or
-    column levels -> 4 + 3), case a keeps the reference split; whole products against GMP."""
+@pytest.mark.parametrize("depth,w,nl,caseb", [(12, 32, 2200000, True), (13, 16, 4500000, True),
+                                              (14, 8, 9000000, True), (13, 16, 3000000, False),
+                                              (16, 2, 30000000, False), (12, 32, 1500000, False),
+                                              (5, 4096, 20000, True), (6, 2048, 40000, True),
+                                              (7, 1024, 80000, True)])
+def test_mfa_split_l2048(mp, oracle, depth, w, nl, caseb):
+    """The plan's MFA split at l = 2048 (make_plan): truncation case b, and case a at depth 13-15
+    (round 6), take twice the reference's columns (mul_fft.c:3195) with four-level forward
+    k_rpass passes (7 row or column levels -> 4 + 3); case a elsewhere keeps the reference split;
+    whole products against GMP."""
     P = mp.plan_info(nl, nl, depth, w)
-    assert P["l"] == 2048 and (P["trunc"] > P["n"]) == alt, P
+    assert P["l"] == 2048 and (P["trunc"] > P["n"]) == caseb, P
+    alt = caseb or 13 <= depth <= 15
     assert P["NC"] == 1 << (depth // 2 + (1 if alt else 0)), P
     a = mp.fill_random(nl, 0x9009 + depth)
     b = mp.fill_random(nl - 5, 0xA00A + w)
