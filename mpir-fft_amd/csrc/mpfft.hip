@@ -316,6 +316,14 @@ static int make_plan(Plan *p, long n1, long n2, unsigned long depth, unsigned lo
     int rc = make_plan_split(p, n1, n2, depth, w, sqrt2, -1);
     // diagnostics (A/B): MPFFT_SPLIT=ref / alt forces a split
     static const char *force = diag_env("MPFFT_SPLIT");
+    // l = 4096, truncation case b: twice the reference's columns since the live-group launches (C4 74.1-74.3
+    // -> 72.2 ms, profiles/r06/c4_split_ab.txt; round 4, before them, measured it slower); case a unmeasured
+    if (!rc && !sqrt2 && p->rpass && p->l == 4096 && !(force && !strcmp(force, "ref"))
+        && (2 * p->Tr > p->NR || (force && !strcmp(force, "alt4")))) {
+        Plan q;
+        if (make_plan_split(&q, n1, n2, depth, w, sqrt2, (int)depth / 2 + 1) == MPFFT_OK && q.rpass) *p = q;
+        return rc;
+    }
     if (rc || sqrt2 || !p->rpass || p->l != 2048 || (force && !strcmp(force, "ref"))) return rc;
     // case a (2 Tr <= NR) too at depth 13-15 since the live-group launches (C2 6.09 -> 5.95 ms, -2.2 to
     // -4.8 % over truncation ratios 0.40-0.48 at depth 13-15, +0.3-0.5 % at depth 16:

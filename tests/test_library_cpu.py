@@ -47,10 +47,11 @@ def test_plan_matches_reference_parameters(mp, oracle):
             P = mp.plan_info(n1, n2, depth, w)
             n, l, sq, j1, j2, trunc, bits1 = oracle.params(n1, n2, depth, w)
             # the MFA split is internal: at l = 2048 make_plan doubles the columns in truncation
-            # case b, and in case a at depth 13-15 (mpfft.hip make_plan)
+            # case b, and in case a at depth 13-15; at l = 4096 in case b (mpfft.hip make_plan)
             # (case a only where the doubled column count's rounding adds at most 1/64 to trunc)
             alt_tr = -(-(j1 + j2 - 1) // (4 * sq)) * 4 * sq
-            alt = l == 2048 and (trunc > n or (13 <= depth <= 15 and alt_tr <= trunc + trunc // 64))
+            alt = (l == 2048 and (trunc > n or (13 <= depth <= 15 and alt_tr <= trunc + trunc // 64))) or \
+                  (l == 4096 and trunc > n)
             assert (P["n"], P["l"], P["NC"], P["j1"], P["j2"], P["trunc"], P["bits1"]) == \
                 (n, l, 2 * sq if alt else sq, j1, j2, alt_tr if alt else trunc, bits1)
             assert P["NR"] * P["NC"] == 2 * n
